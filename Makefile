@@ -1,0 +1,58 @@
+# Build of the MI355X product (libldpc_hip.so + CLI front-ends) and the CPU
+# oracle (test infrastructure). gfx950 only.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+CSRC      = ldpcsimulation_amd/csrc
+LIBDIR    = ldpcsimulation_amd/lib
+BINDIR    = bin
+# -ffp-contract=off: the decoder must not fuse 1+sigma*n or the quantiser
+# into FMAs (bit-exact parity with the reference's plain IEEE arithmetic).
+HIPFLAGS  = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -I$(CSRC) \
+            -Wall -Wno-unused-result
+CXXFLAGS  = -O2 -std=c++17 -ffp-contract=off -Iinclude -Wall
+
+LIB       = $(LIBDIR)/libldpc_hip.so
+OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
+CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalizedMinSum $(BINDIR)/decodeOffsetMinSum
+
+all: $(LIB) $(CLIS) oracle
+
+$(LIBDIR)/obj:
+	mkdir -p $@
+$(BINDIR):
+	mkdir -p $@
+
+$(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h | $(LIBDIR)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+$(LIBDIR)/obj/api.o: $(CSRC)/api.cpp $(CSRC)/kernels.h $(CSRC)/graph.h include/ldpc_hip.h | $(LIBDIR)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+$(LIBDIR)/obj/graph.o: $(CSRC)/graph.cpp $(CSRC)/graph.h | $(LIBDIR)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+# Reference-compatible CLI front-ends: the variant is fixed at compile time
+# exactly as C_implementations/Makefile:58-65 does (plus decodeNMS =
+# -D normalizedMS without quantisation, the BASELINE config-2 variant).
+CLI_SRC = $(CSRC)/cli_minsum.cpp
+CLI_LINK = -L$(LIBDIR) -lldpc_hip -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+$(BINDIR)/decodeMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeNMS: $(CLI_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D normalizedMS -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeNormalizedMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D quantizeSamples -D normalizedMS -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeOffsetMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D quantizeSamples -D offsetMS -o $@ $< $(CLI_LINK)
+
+oracle:
+	$(MAKE) -f oracle/Makefile
+
+ref:
+	@if [ -d /root/reference/C_implementations ]; then $(MAKE) -f oracle/Makefile.ref; \
+	 else echo "reference sources absent: oracle/_ref not rebuilt"; fi
+
+clean:
+	rm -rf $(LIBDIR) $(BINDIR) oracle/liboracle.so
+
+.PHONY: all oracle ref clean

@@ -1,0 +1,182 @@
+/*
+ * ldpc_hip.h -- C ABI of the MI355X-native LDPC min-sum decoder
+ * (libldpc_hip.so, built from ldpcsimulation_amd/csrc/).
+ *
+ * Drop-in boundary for the hot path of ereiss123/LDPCsimulation
+ * (paths relative to C_implementations/):
+ *   - ldpc_graph_create / ldpc_graph_load_alist replace the H-matrix loader
+ *     loadFile() (src/alist.cpp:22-95, inc/alist.h:21-41) and the message
+ *     memory setup setupSymMessages/setupCheckMessages (src/decodeMinSum.cpp
+ *     :345-361). ldpc_graph_create takes exactly the arrays of an
+ *     alist_struct (N, M, num_nlist, nlist, num_mlist, mlist; 1-based,
+ *     zero padded), so an existing loadFile() result passes straight through.
+ *   - ldpc_decode_batch replaces the per-frame decode loop
+ *     initializeSymMessages + T x {checkNodeUpdates, applyNormalization |
+ *     applyOffset, symNodeUpdates} + countDecisionErrors
+ *     (src/decodeMinSum.cpp:240-270, functions at :364-370, :410-515,
+ *     :382-393) for a batch of frames whose channel samples y are given
+ *     (the reference's `y`/`yq` vectors, :214-238).
+ *   - ldpc_sim_launch / ldpc_sim_batch replace the body of the Monte-Carlo
+ *     frame loop (src/decodeMinSum.cpp:189-289: AWGN, quantise/saturate,
+ *     decode, error accounting) with one fused device pass per batch; the
+ *     stop rule (:189) stays with the caller, which reads ldpc_counts.
+ *   The compile-time variants of the reference (-D normalizedMS, offsetMS,
+ *   quantizeSamples, saturateSamples; src/decodeMinSum.cpp:26-32,
+ *   Makefile:58-65) are runtime fields of ldpc_decoder_cfg.
+ *
+ * Conventions: every function returns LDPC_OK (0) or a negative
+ * ldpc_status; ldpc_last_error() gives a thread-local message. No C++
+ * exception crosses the ABI. Buffers may be host or device pointers (the
+ * library checks with hipPointerGetAttributes); the caller owns them and the
+ * library never frees caller memory. A context is not thread-safe: one host
+ * thread (or process) per GPU. Graphs are immutable after creation and may
+ * be shared read-only between contexts.
+ */
+#ifndef LDPC_HIP_H
+#define LDPC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDPC_ABI_VERSION 1
+
+typedef enum {
+    LDPC_OK = 0,
+    LDPC_ERR_INVALID = -1,     /* bad argument                         */
+    LDPC_ERR_NOMEM = -2,       /* host or device allocation failed     */
+    LDPC_ERR_DEVICE = -3,      /* HIP runtime / kernel error           */
+    LDPC_ERR_UNSUPPORTED = -4, /* shape or option not supported        */
+    LDPC_ERR_IO = -5,          /* file could not be read               */
+    LDPC_ERR_GRAPH = -6        /* inconsistent / malformed H matrix    */
+} ldpc_status;
+
+/* Check-node rule: MS = decodeMinSum, NMS = -D normalizedMS (c2v /= alpha,
+ * src/decodeMinSum.cpp:494-499), OMS = -D offsetMS (:503-515). */
+typedef enum { LDPC_MS = 0, LDPC_NMS = 1, LDPC_OMS = 2 } ldpc_variant;
+
+/* Message arithmetic. F64 is the reference's own precision and reproduces
+ * its decisions bit-for-bit for identical y; F32 is the throughput path. */
+typedef enum { LDPC_F32 = 0, LDPC_F64 = 1 } ldpc_precision;
+
+typedef struct ldpc_graph ldpc_graph;
+typedef struct ldpc_ctx ldpc_ctx;
+
+/* Error accounting of src/decodeMinSum.cpp:167-172,270-288, int64 as the
+ * reference's `long` counters, plus a syndrome check (H*d != 0). */
+typedef struct {
+    int64_t bit_err;         /* errors          */
+    int64_t frame_err;       /* wordErrors      */
+    int64_t uncoded_bit_err; /* uncodedErrors   */
+    int64_t frames;          /* totalWords      */
+    int64_t iters;           /* totalIterations */
+    int64_t syndrome_fail;   /* frames whose hard decision is not a codeword */
+} ldpc_counts;
+
+/* Per-frame outcome (optional output), in frame order. */
+typedef struct {
+    int32_t bit_err;          /* newErrors of :270 (0 = frame decoded)  */
+    int32_t uncoded_bit_err;  /* hard-decision errors before decoding    */
+    int32_t syndrome_fail;    /* 1 if H*d != 0                          */
+    int32_t reserved;
+} ldpc_frame_result;
+
+typedef struct {
+    int32_t variant;    /* ldpc_variant                                     */
+    int32_t precision;  /* ldpc_precision                                   */
+    int32_t T;          /* iterations (num_iterations), fixed, no early stop */
+    int32_t quantize;   /* -D quantizeSamples: quantize(y, ymax, 2^qbits)   */
+    int32_t saturate;   /* -D saturateSamples: clip at +-ymax               */
+    int32_t qbits;      /* Q                                                */
+    double  ymax;       /* Ymax                                             */
+    double  alpha;      /* NMS divisor                                      */
+    double  delta;      /* OMS offset                                       */
+} ldpc_decoder_cfg;
+
+int         ldpc_abi_version(void);
+const char *ldpc_last_error(void);
+
+/* ---- graph (H matrix) ------------------------------------------------ */
+/* Arrays exactly as alist_struct (inc/alist.h:21-36): nlist[i] has
+ * num_nlist[i] 1-based check indices of bit i, mlist[j] has num_mlist[j]
+ * 1-based bit indices of check j (entries beyond the weight are ignored).
+ * Validates that both views describe the same edge set. */
+int  ldpc_graph_create(int N, int M, const int *num_nlist, const int *const *nlist,
+                       const int *num_mlist, const int *const *mlist, ldpc_graph **out);
+/* MacKay alist file with the reference loader's fixed-width semantics
+ * (src/alist.cpp:70-93). */
+int  ldpc_graph_load_alist(const char *path, ldpc_graph **out);
+int  ldpc_graph_info(const ldpc_graph *g, int *N, int *M, int *E, int *maxdv, int *maxdc);
+void ldpc_graph_destroy(ldpc_graph *g);
+
+/* ---- device context --------------------------------------------------- */
+int  ldpc_device_count(int *n);
+/* One per device: uploads the graph, owns a HIP stream, counters, scratch.
+ * max_batch bounds the frames of one decode/sim call. */
+int  ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **out);
+/* Launch on an external hipStream_t (e.g. torch.cuda.current_stream()); NULL
+ * restores the context's own stream. */
+int  ldpc_ctx_set_stream(ldpc_ctx *ctx, void *hip_stream);
+int  ldpc_ctx_synchronize(ldpc_ctx *ctx);
+void ldpc_ctx_destroy(ldpc_ctx *ctx);
+
+/* Decode `batch` frames of given channel samples y[batch][N] (float for
+ * LDPC_F32, double for LDPC_F64; host or device). The cfg front-end
+ * (quantize / saturate) is applied to y first, as :218-229 does.
+ * c: transmitted bipolar codewords [batch][N] (+1/-1, int8) or NULL for the
+ *    all-zero codeword (c = +1, :159).
+ * d_out [batch][N] int8 +1/-1 decisions and frames [batch] per-frame
+ * results: optional (NULL). counts: optional, ACCUMULATED (+=). Synchronous. */
+int  ldpc_decode_batch(ldpc_ctx *ctx, const void *y, int batch, const ldpc_decoder_cfg *cfg,
+                       const int8_t *c, int8_t *d_out, ldpc_frame_result *frames,
+                       ldpc_counts *counts);
+
+/* Codeword-file mode (:136-143, :193-212): rows of 0/1 bits [rows][N];
+ * frame with global index f transmits row f % rows. rows = 0 restores the
+ * all-zero codeword. */
+int  ldpc_sim_set_codewords(ldpc_ctx *ctx, const uint8_t *bits, int rows);
+
+/* Fused on-device Monte-Carlo of one SNR point: BPSK, AWGN with
+ * sigma = sqrt(10^(-ebn0/10)/R/2) (:146-147) from counter-based
+ * Philox4x32-10 keyed by (seed, stream_id, global frame index, bit index),
+ * front-end, T iterations, error accounting into the context's device
+ * counters. Frames first_cw .. first_cw+batch-1; the result does not depend
+ * on how frames are split across calls or devices. Asynchronous.
+ * frames_dev: optional DEVICE pointer [batch] of per-frame results. */
+int  ldpc_sim_launch(ldpc_ctx *ctx, double ebn0_db, double R, const ldpc_decoder_cfg *cfg,
+                     uint64_t seed, uint32_t stream_id, uint64_t first_cw, int batch,
+                     ldpc_frame_result *frames_dev);
+/* Synchronising read of the accumulated device counters (reset != 0 zeroes them). */
+int  ldpc_ctx_read_counts(ldpc_ctx *ctx, ldpc_counts *out, int reset);
+/* Error-weight histogram (error_weight_hist, :173,:280): out[w-1] = frames
+ * with w bit errors, N entries. */
+int  ldpc_ctx_read_histogram(ldpc_ctx *ctx, int64_t *out, int reset);
+/* ldpc_sim_launch + the batch's counts accumulated into *accum; frames
+ * (optional) may be host or device. Synchronous. */
+int  ldpc_sim_batch(ldpc_ctx *ctx, double ebn0_db, double R, const ldpc_decoder_cfg *cfg,
+                    uint64_t seed, uint32_t stream_id, uint64_t first_cw, int batch,
+                    ldpc_frame_result *frames, ldpc_counts *accum);
+
+/* ldpc_sim_batch that also returns what the fused kernel generated: the
+ * channel samples y_out [batch][N] (float for F32, double for F64, before
+ * the front-end) and the decisions d_out [batch][N] (+1/-1). Either may be
+ * NULL; host or device. For verification of the on-device channel. */
+int  ldpc_sim_trace(ldpc_ctx *ctx, double ebn0_db, double R, const ldpc_decoder_cfg *cfg,
+                    uint64_t seed, uint32_t stream_id, uint64_t first_cw, int batch,
+                    void *y_out, int8_t *d_out, ldpc_frame_result *frames, ldpc_counts *accum);
+
+/* Device time (ms) of the last decode kernel, from HIP events recorded on
+ * the launch stream around it. Synchronises that stream. */
+int  ldpc_ctx_last_kernel_ms(ldpc_ctx *ctx, float *ms);
+/* Kernel chosen for a cfg ("lds" / "global") and its per-codeword LDS bytes.
+ * The environment variable LDPC_FORCE_GLOBAL=1 (read at ldpc_ctx_create)
+ * forces the global-memory kernel, for testing it on small codes. */
+int  ldpc_ctx_kernel_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, char *name, int name_len,
+                          int *lds_bytes, int *blocks_per_cu);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDPC_HIP_H */

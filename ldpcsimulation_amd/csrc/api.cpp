@@ -1,0 +1,630 @@
+// api.cpp -- C ABI of libldpc_hip.so (include/ldpc_hip.h).
+//
+// Owns device state (graph upload, counters, staging buffers, events) and
+// maps the reference's per-frame loop onto batched kernel launches. No C++
+// exception crosses the ABI; every HIP failure becomes LDPC_ERR_DEVICE with
+// a message in ldpc_last_error().
+#include "ldpc_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdlib>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "graph.h"
+#include "kernels.h"
+
+static thread_local std::string g_last_error;
+
+static int set_err(int code, const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                           \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess) {                                                                 \
+            (void)hipGetLastError();                                                            \
+            return set_err(LDPC_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                           __FILE__, __LINE__);                                                 \
+        }                                                                                       \
+    } while (0)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes)
+    {
+        if (bytes <= n) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) n = bytes;
+        return e;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct ldpc_ctx {
+    int device = 0;
+    const ldpc_graph *g = nullptr;
+    int max_batch = 0;
+    int num_cus = 0;
+    hipStream_t own = nullptr, stream = nullptr;
+    ldpc::DevGraph dg{};
+    DevBuf graph, counts, hist, y_stage, c_stage, d_stage, fw_stage, cw_table, gscratch;
+    int cw_rows = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    char force[16] = {0};        // LDPC_KERNEL=lds|global (LDPC_FORCE_GLOBAL=1 = global), tests only
+    bool has_rs = false;
+    ldpc::RowSched rs{};
+    DevBuf sched;
+};
+
+extern "C" {
+
+int ldpc_abi_version(void) { return LDPC_ABI_VERSION; }
+const char *ldpc_last_error(void) { return g_last_error.c_str(); }
+
+// ----------------------------------------------------------------- graph
+int ldpc_graph_create(int N, int M, const int *num_nlist, const int *const *nlist, const int *num_mlist,
+                      const int *const *mlist, ldpc_graph **out)
+{
+    if (!out) return set_err(LDPC_ERR_INVALID, "out is null");
+    *out = nullptr;
+    ldpc_graph *g = new (std::nothrow) ldpc_graph();
+    if (!g) return set_err(LDPC_ERR_NOMEM, "graph allocation failed");
+    std::string err;
+    try {
+        err = ldpc::build_graph(N, M, num_nlist, nlist, num_mlist, mlist, *g);
+    } catch (const std::bad_alloc &) {
+        delete g;
+        return set_err(LDPC_ERR_NOMEM, "graph build out of memory");
+    }
+    if (!err.empty()) {
+        delete g;
+        return set_err(LDPC_ERR_GRAPH, "%s", err.c_str());
+    }
+    *out = g;
+    return LDPC_OK;
+}
+
+int ldpc_graph_load_alist(const char *path, ldpc_graph **out)
+{
+    if (!out || !path) return set_err(LDPC_ERR_INVALID, "null argument");
+    *out = nullptr;
+    ldpc_graph *g = new (std::nothrow) ldpc_graph();
+    if (!g) return set_err(LDPC_ERR_NOMEM, "graph allocation failed");
+    std::string err;
+    try {
+        err = ldpc::load_alist(path, *g);
+    } catch (const std::bad_alloc &) {
+        delete g;
+        return set_err(LDPC_ERR_NOMEM, "alist load out of memory");
+    }
+    if (!err.empty()) {
+        delete g;
+        const bool io = err.rfind("cannot open", 0) == 0;
+        return set_err(io ? LDPC_ERR_IO : LDPC_ERR_GRAPH, "%s", err.c_str());
+    }
+    *out = g;
+    return LDPC_OK;
+}
+
+int ldpc_graph_info(const ldpc_graph *g, int *N, int *M, int *E, int *maxdv, int *maxdc)
+{
+    if (!g) return set_err(LDPC_ERR_INVALID, "graph is null");
+    if (N) *N = g->N;
+    if (M) *M = g->M;
+    if (E) *E = g->E;
+    if (maxdv) *maxdv = g->maxdv;
+    if (maxdc) *maxdc = g->maxdc;
+    return LDPC_OK;
+}
+
+void ldpc_graph_destroy(ldpc_graph *g) { delete g; }
+
+// ----------------------------------------------------------------- context
+int ldpc_device_count(int *n)
+{
+    if (!n) return set_err(LDPC_ERR_INVALID, "n is null");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *n = 0;
+        return set_err(LDPC_ERR_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *n = c;
+    return LDPC_OK;
+}
+
+static void ctx_free(ldpc_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (DevBuf *b : {&c->graph, &c->counts, &c->hist, &c->y_stage, &c->c_stage, &c->d_stage, &c->fw_stage,
+                      &c->cw_table, &c->gscratch, &c->sched})
+        b->release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **out)
+{
+    if (!out || !g) return set_err(LDPC_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (max_batch <= 0) return set_err(LDPC_ERR_INVALID, "max_batch must be > 0");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return set_err(LDPC_ERR_INVALID, "device %d of %d", device, ndev);
+    ldpc_ctx *c = new (std::nothrow) ldpc_ctx();
+    if (!c) return set_err(LDPC_ERR_NOMEM, "ctx allocation failed");
+    c->device = device;
+    c->g = g;
+    c->max_batch = max_batch;
+    {
+        const char *fg = std::getenv("LDPC_FORCE_GLOBAL");
+        const char *fk = std::getenv("LDPC_KERNEL");
+        if (fg && fg[0] == '1') std::snprintf(c->force, sizeof c->force, "global");
+        else if (fk) std::snprintf(c->force, sizeof c->force, "%s", fk);
+    }
+    auto fail = [&](int rc) {
+        ctx_free(c);
+        return rc;
+    };
+    hipError_t e;
+#define CTX_TRY(expr)                                                                                   \
+    do {                                                                                                \
+        e = (expr);                                                                                     \
+        if (e != hipSuccess) {                                                                          \
+            (void)hipGetLastError();                                                                    \
+            return fail(set_err(LDPC_ERR_DEVICE, "%s failed: %s", #expr, hipGetErrorString(e)));       \
+        }                                                                                               \
+    } while (0)
+    CTX_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    CTX_TRY(hipGetDeviceProperties(&prop, device));
+    c->num_cus = prop.multiProcessorCount;
+    CTX_TRY(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+    c->stream = c->own;
+    CTX_TRY(hipEventCreate(&c->ev0));
+    CTX_TRY(hipEventCreate(&c->ev1));
+
+    // Graph upload: one allocation, 256-B aligned sections.
+    const int dcs = g->maxdc > 0 ? g->maxdc : 1;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t s_rc = al(sizeof(int32_t) * (size_t)g->M * dcs), s_rd = al((size_t)g->M),
+                 s_cp = al(sizeof(int32_t) * (size_t)(g->N + 1)), s_cr = al(sizeof(uint32_t) * (size_t)(g->E + 1));
+    CTX_TRY(c->graph.ensure(s_rc + s_rd + s_cp + s_cr));
+    unsigned char *gb = (unsigned char *)c->graph.p;
+    CTX_TRY(hipMemcpy(gb, g->row_cols.data(), sizeof(int32_t) * g->row_cols.size(), hipMemcpyHostToDevice));
+    CTX_TRY(hipMemcpy(gb + s_rc, g->row_deg.data(), g->row_deg.size(), hipMemcpyHostToDevice));
+    CTX_TRY(hipMemcpy(gb + s_rc + s_rd, g->col_ptr.data(), sizeof(int32_t) * g->col_ptr.size(),
+                      hipMemcpyHostToDevice));
+    if (g->E > 0)
+        CTX_TRY(hipMemcpy(gb + s_rc + s_rd + s_cp, g->col_refs.data(), sizeof(uint32_t) * g->col_refs.size(),
+                          hipMemcpyHostToDevice));
+    c->dg.N = g->N;
+    c->dg.M = g->M;
+    c->dg.dcs = dcs;
+    c->dg.row_cols = (const int32_t *)gb;
+    c->dg.row_deg = (const uint8_t *)(gb + s_rc);
+    c->dg.col_ptr = (const int32_t *)(gb + s_rc + s_rd);
+    c->dg.col_refs = (const uint32_t *)(gb + s_rc + s_rd + s_cp);
+
+    // Row-parallel schedule (the throughput kernel) when the graph fits it.
+    {
+        int threads = ((g->M + 63) / 64) * 64;
+        if (threads < 64) threads = 64;
+        int dc = 0, cpt = 0;
+        for (int d : ldpc::kRowsDc)
+            if (!dc && g->maxdc <= d) dc = d;
+        for (int q : ldpc::kRowsCpt)
+            if (!cpt && (long)threads * q >= g->N) cpt = q;
+        ldpc::RowSchedule hs;
+        if (threads <= ldpc::kRowsMaxThreads && dc && cpt && ldpc::build_row_schedule(*g, threads, cpt, dc, hs).empty()) {
+            const size_t b_cc = al(2 * hs.cn_cols.size()), b_cp = al(2 * hs.cn_pos.size()), b_cd = al(hs.cn_deg.size()),
+                         b_vc = al(2 * hs.vn_col.size()), b_vi = al(4 * hs.vn_info.size());
+            CTX_TRY(c->sched.ensure(b_cc + b_cp + b_cd + b_vc + b_vi));
+            unsigned char *sb = (unsigned char *)c->sched.p;
+            CTX_TRY(hipMemcpy(sb, hs.cn_cols.data(), 2 * hs.cn_cols.size(), hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(sb + b_cc, hs.cn_pos.data(), 2 * hs.cn_pos.size(), hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(sb + b_cc + b_cp, hs.cn_deg.data(), hs.cn_deg.size(), hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(sb + b_cc + b_cp + b_cd, hs.vn_col.data(), 2 * hs.vn_col.size(), hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(sb + b_cc + b_cp + b_cd + b_vc, hs.vn_info.data(), 4 * hs.vn_info.size(),
+                              hipMemcpyHostToDevice));
+            c->rs.threads = hs.threads;
+            c->rs.cpt = hs.cpt;
+            c->rs.dc = hs.dc;
+            c->rs.e_pad = hs.e_pad;
+            c->rs.cn_cols = (const uint16_t *)sb;
+            c->rs.cn_pos = (const uint16_t *)(sb + b_cc);
+            c->rs.cn_deg = (const uint8_t *)(sb + b_cc + b_cp);
+            c->rs.vn_col = (const uint16_t *)(sb + b_cc + b_cp + b_cd);
+            c->rs.vn_info = (const uint32_t *)(sb + b_cc + b_cp + b_cd + b_vc);
+            c->has_rs = true;
+        }
+    }
+    CTX_TRY(c->counts.ensure(8 * sizeof(unsigned long long)));
+    CTX_TRY(hipMemset(c->counts.p, 0, c->counts.n));
+    CTX_TRY(c->hist.ensure(sizeof(unsigned long long) * (size_t)g->N));
+    CTX_TRY(hipMemset(c->hist.p, 0, c->hist.n));
+#undef CTX_TRY
+    *out = c;
+    return LDPC_OK;
+}
+
+int ldpc_ctx_set_stream(ldpc_ctx *c, void *s)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    c->stream = s ? (hipStream_t)s : c->own;
+    return LDPC_OK;
+}
+
+int ldpc_ctx_synchronize(ldpc_ctx *c)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return LDPC_OK;
+}
+
+void ldpc_ctx_destroy(ldpc_ctx *c) { ctx_free(c); }
+
+// ----------------------------------------------------------------- helpers
+static bool is_device_ptr(const void *p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+static int check_cfg(const ldpc_ctx *c, const ldpc_decoder_cfg *cfg)
+{
+    if (!cfg) return set_err(LDPC_ERR_INVALID, "cfg is null");
+    if (cfg->variant < LDPC_MS || cfg->variant > LDPC_OMS) return set_err(LDPC_ERR_INVALID, "bad variant %d", cfg->variant);
+    if (cfg->precision != LDPC_F32 && cfg->precision != LDPC_F64)
+        return set_err(LDPC_ERR_INVALID, "bad precision %d", cfg->precision);
+    if (cfg->T < 0) return set_err(LDPC_ERR_INVALID, "T must be >= 0");
+    if ((cfg->quantize || cfg->saturate) && !(cfg->ymax > 0))
+        return set_err(LDPC_ERR_INVALID, "quantize/saturate need ymax > 0");
+    if (cfg->quantize && (cfg->qbits < 1 || cfg->qbits > 30)) return set_err(LDPC_ERR_INVALID, "qbits out of range");
+    (void)c;
+    return LDPC_OK;
+}
+
+static void fill_common(ldpc::DecodeArgs &a, ldpc_ctx *c, const ldpc_decoder_cfg *cfg, int batch)
+{
+    std::memset(&a, 0, sizeof a);
+    a.batch = batch;
+    a.T = cfg->T;
+    a.variant = cfg->variant;
+    a.quantize = cfg->quantize;
+    a.saturate = cfg->saturate;
+    a.ymax = cfg->ymax;
+    a.nq = std::pow(2.0, (double)cfg->qbits);   // Nq = pow(2.0, Q) (:121)
+    a.alpha = cfg->alpha;
+    a.delta = cfg->delta;
+    a.counts = (unsigned long long *)c->counts.p;
+    a.hist = (unsigned long long *)c->hist.p;
+}
+
+static_assert(sizeof(ldpc_frame_result) == sizeof(int4), "frame result layout");
+
+static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64)
+{
+    const ldpc::KernelChoice kc =
+        ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr);
+    int gblocks = 0;
+    if (kc.scratch_per_block) {
+        int per_cu = ldpc::blocks_per_cu(c->dg, f64, kc);
+        if (per_cu <= 0) per_cu = 1;
+        gblocks = per_cu * c->num_cus;
+        if (gblocks > a.batch) gblocks = a.batch;
+        HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks));
+    }
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream, c->has_rs ? &c->rs : nullptr,
+                                c->num_cus));
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return LDPC_OK;
+}
+
+static int read_counts(ldpc_ctx *c, ldpc_counts *out, int reset)
+{
+    unsigned long long h[8];
+    HIP_TRY(hipMemcpyAsync(h, c->counts.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (out) {
+        out->bit_err = (int64_t)h[0];
+        out->frame_err = (int64_t)h[1];
+        out->uncoded_bit_err = (int64_t)h[2];
+        out->frames = (int64_t)h[3];
+        out->iters = (int64_t)h[4];
+        out->syndrome_fail = (int64_t)h[5];
+    }
+    if (reset) HIP_TRY(hipMemsetAsync(c->counts.p, 0, c->counts.n, c->stream));
+    return LDPC_OK;
+}
+
+static void accumulate(ldpc_counts *acc, const ldpc_counts &d)
+{
+    acc->bit_err += d.bit_err;
+    acc->frame_err += d.frame_err;
+    acc->uncoded_bit_err += d.uncoded_bit_err;
+    acc->frames += d.frames;
+    acc->iters += d.iters;
+    acc->syndrome_fail += d.syndrome_fail;
+}
+
+// ----------------------------------------------------------------- decode
+int ldpc_decode_batch(ldpc_ctx *c, const void *y, int batch, const ldpc_decoder_cfg *cfg, const int8_t *cw,
+                      int8_t *d_out, ldpc_frame_result *frame_weights, ldpc_counts *counts)
+{
+    if (!c || !y) return set_err(LDPC_ERR_INVALID, "null argument");
+    int rc = check_cfg(c, cfg);
+    if (rc) return rc;
+    if (batch <= 0 || batch > c->max_batch)
+        return set_err(LDPC_ERR_INVALID, "batch %d outside 1..max_batch=%d", batch, c->max_batch);
+    HIP_TRY(hipSetDevice(c->device));
+    const bool f64 = cfg->precision == LDPC_F64;
+    const int N = c->g->N;
+    const size_t ybytes = (size_t)batch * N * (f64 ? 8 : 4);
+    const size_t nbytes = (size_t)batch * N;
+
+    ldpc::DecodeArgs a;
+    fill_common(a, c, cfg, batch);
+    a.src = ldpc::SRC_GIVEN;
+    // Inputs: stage host buffers.
+    if (is_device_ptr(y)) {
+        a.y = y;
+    } else {
+        HIP_TRY(c->y_stage.ensure(ybytes));
+        HIP_TRY(hipMemcpyAsync(c->y_stage.p, y, ybytes, hipMemcpyHostToDevice, c->stream));
+        a.y = c->y_stage.p;
+    }
+    if (cw) {
+        if (is_device_ptr(cw)) {
+            a.c = cw;
+        } else {
+            HIP_TRY(c->c_stage.ensure(nbytes));
+            HIP_TRY(hipMemcpyAsync(c->c_stage.p, cw, nbytes, hipMemcpyHostToDevice, c->stream));
+            a.c = (const int8_t *)c->c_stage.p;
+        }
+    }
+    const bool d_host = d_out && !is_device_ptr(d_out);
+    const bool w_host = frame_weights && !is_device_ptr(frame_weights);
+    if (d_host) {
+        HIP_TRY(c->d_stage.ensure(nbytes));
+        a.d_out = (int8_t *)c->d_stage.p;
+    } else {
+        a.d_out = d_out;
+    }
+    if (w_host) {
+        HIP_TRY(c->fw_stage.ensure(sizeof(ldpc_frame_result) * (size_t)batch));
+        a.frame_res = (int4 *)c->fw_stage.p;
+    } else {
+        a.frame_res = (int4 *)frame_weights;
+    }
+    ldpc_counts before;
+    rc = read_counts(c, &before, 0);
+    if (rc) return rc;
+    rc = run_kernel(c, a, f64);
+    if (rc) return rc;
+    if (d_host) HIP_TRY(hipMemcpyAsync(d_out, c->d_stage.p, nbytes, hipMemcpyDeviceToHost, c->stream));
+    if (w_host)
+        HIP_TRY(hipMemcpyAsync(frame_weights, c->fw_stage.p, sizeof(ldpc_frame_result) * (size_t)batch,
+                               hipMemcpyDeviceToHost, c->stream));
+    ldpc_counts after;
+    rc = read_counts(c, &after, 0);
+    if (rc) return rc;
+    if (counts) {
+        ldpc_counts d;
+        d.bit_err = after.bit_err - before.bit_err;
+        d.frame_err = after.frame_err - before.frame_err;
+        d.uncoded_bit_err = after.uncoded_bit_err - before.uncoded_bit_err;
+        d.frames = after.frames - before.frames;
+        d.iters = after.iters - before.iters;
+        d.syndrome_fail = after.syndrome_fail - before.syndrome_fail;
+        accumulate(counts, d);
+    }
+    return LDPC_OK;
+}
+
+// ----------------------------------------------------------------- Monte-Carlo
+int ldpc_sim_set_codewords(ldpc_ctx *c, const uint8_t *bits, int rows)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    if (rows < 0 || (rows > 0 && !bits)) return set_err(LDPC_ERR_INVALID, "bad codeword table");
+    HIP_TRY(hipSetDevice(c->device));
+    c->cw_rows = 0;
+    if (rows == 0) return LDPC_OK;
+    const size_t n = (size_t)rows * c->g->N;
+    std::vector<int8_t> bip(n);
+    for (size_t i = 0; i < n; ++i) {
+        if (bits[i] > 1) return set_err(LDPC_ERR_INVALID, "codeword bit %zu is %d (want 0/1)", i, bits[i]);
+        bip[i] = bits[i] ? -1 : +1;   // '1' -> c = -1, '0' -> c = +1 (:204-207)
+    }
+    HIP_TRY(c->cw_table.ensure(n));
+    HIP_TRY(hipMemcpy(c->cw_table.p, bip.data(), n, hipMemcpyHostToDevice));
+    c->cw_rows = rows;
+    return LDPC_OK;
+}
+
+static int sim_launch_impl(ldpc_ctx *c, double ebn0_db, double R, const ldpc_decoder_cfg *cfg, uint64_t seed,
+                           uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames_dev,
+                           void *y_out_dev, int8_t *d_out_dev)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    int rc = check_cfg(c, cfg);
+    if (rc) return rc;
+    if (batch <= 0 || batch > c->max_batch)
+        return set_err(LDPC_ERR_INVALID, "batch %d outside 1..max_batch=%d", batch, c->max_batch);
+    if (!(R > 0)) return set_err(LDPC_ERR_INVALID, "rate must be > 0");
+    HIP_TRY(hipSetDevice(c->device));
+    ldpc::DecodeArgs a;
+    fill_common(a, c, cfg, batch);
+    a.src = ldpc::SRC_PHILOX;
+    const double N0 = std::pow(10.0, -ebn0_db / 10.0) / R;   // :146
+    a.sigma = std::sqrt(N0 / 2.0);                            // :147
+    a.seed = seed;
+    a.stream_id = stream_id;
+    a.first_cw = first_cw;
+    a.cw_table = c->cw_rows ? (const int8_t *)c->cw_table.p : nullptr;
+    a.cw_rows = c->cw_rows;
+    a.frame_res = (int4 *)frames_dev;
+    a.y_out = y_out_dev;
+    a.d_out = d_out_dev;
+    return run_kernel(c, a, cfg->precision == LDPC_F64);
+}
+
+int ldpc_sim_launch(ldpc_ctx *c, double ebn0_db, double R, const ldpc_decoder_cfg *cfg, uint64_t seed,
+                    uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames_dev)
+{
+    if (frames_dev && !is_device_ptr(frames_dev))
+        return set_err(LDPC_ERR_INVALID, "frames_dev must be a device pointer");
+    return sim_launch_impl(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, frames_dev, nullptr, nullptr);
+}
+
+int ldpc_ctx_read_counts(ldpc_ctx *c, ldpc_counts *out, int reset)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    HIP_TRY(hipSetDevice(c->device));
+    return read_counts(c, out, reset);
+}
+
+int ldpc_ctx_read_histogram(ldpc_ctx *c, int64_t *out, int reset)
+{
+    if (!c || !out) return set_err(LDPC_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipMemcpyAsync(out, c->hist.p, c->hist.n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (reset) HIP_TRY(hipMemsetAsync(c->hist.p, 0, c->hist.n, c->stream));
+    return LDPC_OK;
+}
+
+// Synchronous sim with optional host-or-device outputs (staged when host).
+static int sim_sync_impl(ldpc_ctx *c, double ebn0_db, double R, const ldpc_decoder_cfg *cfg, uint64_t seed,
+                         uint32_t stream_id, uint64_t first_cw, int batch, void *y_out, int8_t *d_out,
+                         ldpc_frame_result *frames, ldpc_counts *accum)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    int rc = check_cfg(c, cfg);
+    if (rc) return rc;
+    if (batch <= 0 || batch > c->max_batch)
+        return set_err(LDPC_ERR_INVALID, "batch %d outside 1..max_batch=%d", batch, c->max_batch);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t nb = (size_t)batch * c->g->N;
+    const size_t ybytes = nb * (cfg->precision == LDPC_F64 ? 8 : 4);
+    ldpc_counts before;
+    rc = read_counts(c, &before, 0);
+    if (rc) return rc;
+    const bool w_host = frames && !is_device_ptr(frames);
+    const bool y_host = y_out && !is_device_ptr(y_out);
+    const bool d_host = d_out && !is_device_ptr(d_out);
+    ldpc_frame_result *fw_dev = frames;
+    void *y_dev = y_out;
+    int8_t *d_dev = d_out;
+    if (w_host) {
+        HIP_TRY(c->fw_stage.ensure(sizeof(ldpc_frame_result) * (size_t)batch));
+        fw_dev = (ldpc_frame_result *)c->fw_stage.p;
+    }
+    if (y_host) {
+        HIP_TRY(c->y_stage.ensure(ybytes));
+        y_dev = c->y_stage.p;
+    }
+    if (d_host) {
+        HIP_TRY(c->d_stage.ensure(nb));
+        d_dev = (int8_t *)c->d_stage.p;
+    }
+    rc = sim_launch_impl(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, fw_dev, y_dev, d_dev);
+    if (rc) return rc;
+    if (w_host)
+        HIP_TRY(hipMemcpyAsync(frames, fw_dev, sizeof(ldpc_frame_result) * (size_t)batch, hipMemcpyDeviceToHost,
+                               c->stream));
+    if (y_host) HIP_TRY(hipMemcpyAsync(y_out, y_dev, ybytes, hipMemcpyDeviceToHost, c->stream));
+    if (d_host) HIP_TRY(hipMemcpyAsync(d_out, d_dev, nb, hipMemcpyDeviceToHost, c->stream));
+    ldpc_counts after;
+    rc = read_counts(c, &after, 0);
+    if (rc) return rc;
+    if (accum) {
+        ldpc_counts d;
+        d.bit_err = after.bit_err - before.bit_err;
+        d.frame_err = after.frame_err - before.frame_err;
+        d.uncoded_bit_err = after.uncoded_bit_err - before.uncoded_bit_err;
+        d.frames = after.frames - before.frames;
+        d.iters = after.iters - before.iters;
+        d.syndrome_fail = after.syndrome_fail - before.syndrome_fail;
+        accumulate(accum, d);
+    }
+    return LDPC_OK;
+}
+
+int ldpc_sim_batch(ldpc_ctx *c, double ebn0_db, double R, const ldpc_decoder_cfg *cfg, uint64_t seed,
+                   uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames, ldpc_counts *accum)
+{
+    return sim_sync_impl(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, nullptr, nullptr, frames, accum);
+}
+
+int ldpc_sim_trace(ldpc_ctx *c, double ebn0_db, double R, const ldpc_decoder_cfg *cfg, uint64_t seed,
+                   uint32_t stream_id, uint64_t first_cw, int batch, void *y_out, int8_t *d_out,
+                   ldpc_frame_result *frames, ldpc_counts *accum)
+{
+    return sim_sync_impl(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, y_out, d_out, frames, accum);
+}
+
+int ldpc_ctx_last_kernel_ms(ldpc_ctx *c, float *ms)
+{
+    if (!c || !ms) return set_err(LDPC_ERR_INVALID, "null argument");
+    if (!c->timed) return set_err(LDPC_ERR_INVALID, "no kernel launched yet");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return LDPC_OK;
+}
+
+int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, int name_len, int *lds_bytes,
+                         int *bpc)
+{
+    if (!c || !cfg) return set_err(LDPC_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    const bool f64 = cfg->precision == LDPC_F64;
+    const ldpc::KernelChoice kc =
+        ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr);
+    if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", kc.name);
+    if (lds_bytes) *lds_bytes = kc.lds_bytes;
+    if (bpc) *bpc = ldpc::blocks_per_cu(c->dg, f64, kc);
+    return LDPC_OK;
+}
+
+}  // extern "C"

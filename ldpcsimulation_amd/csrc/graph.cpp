@@ -1,0 +1,177 @@
+// graph.cpp -- host-side Tanner-graph compiler and alist reader.
+// See graph.h. Reference behaviour followed:
+//   loadFile (C_implementations/src/alist.cpp:70-93): header "N M",
+//   "maxdv maxdc", N column weights, M row weights, then exactly
+//   N*maxdv and M*maxdc whitespace-separated 1-based indices (0 = pad),
+//   read by fread_imatrix (src/r.cpp:277-300) irrespective of line breaks.
+// Unlike the reference (which never validates and segfaults on the broken
+// 802.11n files) every index and the row/column agreement is
+// checked here; a malformed H is an LDPC_ERR_GRAPH, not undefined behaviour.
+#include "graph.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <unordered_map>
+
+namespace ldpc {
+
+static std::string fmt(const char *f, long a = 0, long b = 0, long c = 0)
+{
+    char buf[256];
+    std::snprintf(buf, sizeof buf, f, a, b, c);
+    return buf;
+}
+
+std::string build_graph(int N, int M, const int *num_nlist, const int *const *nlist,
+                        const int *num_mlist, const int *const *mlist, ldpc_graph &g)
+{
+    if (N <= 0 || M <= 0) return fmt("bad dimensions N=%ld M=%ld", N, M);
+    if (!num_nlist || !nlist || !num_mlist || !mlist) return "null alist array";
+    g = ldpc_graph();
+    g.N = N;
+    g.M = M;
+    long E_rows = 0, E_cols = 0;
+    for (int j = 0; j < M; ++j) {
+        const int d = num_mlist[j];
+        if (d < 0 || d > kMaxRowDegree)
+            return fmt("check %ld has degree %ld (supported 0..%ld)", j, d, kMaxRowDegree);
+        E_rows += d;
+        g.maxdc = std::max(g.maxdc, d);
+    }
+    for (int i = 0; i < N; ++i) {
+        const int d = num_nlist[i];
+        if (d < 0 || d > 255) return fmt("bit %ld has degree %ld", i, d);
+        E_cols += d;
+        g.maxdv = std::max(g.maxdv, d);
+    }
+    if (E_rows != E_cols)
+        return fmt("row weights sum to %ld but column weights to %ld", E_rows, E_cols);
+    g.E = (int)E_rows;
+    const int dcs = std::max(g.maxdc, 1);
+
+    // Row view (mlist order) + position lookup for the column view.
+    g.row_cols.assign((size_t)M * dcs, 0);
+    g.row_deg.resize(M);
+    std::vector<std::unordered_map<int, int>> pos(M);
+    for (int j = 0; j < M; ++j) {
+        g.row_deg[j] = (uint8_t)num_mlist[j];
+        for (int k = 0; k < num_mlist[j]; ++k) {
+            const int i = mlist[j][k] - 1;
+            if (i < 0 || i >= N) return fmt("check %ld lists bit %ld (out of 1..N)", j, i + 1);
+            g.row_cols[(size_t)j * dcs + k] = i;
+            if (pos[j].count(i)) return fmt("check %ld lists bit %ld twice", j, i + 1);
+            pos[j][i] = k;
+        }
+    }
+    // Column view (nlist order) -> (check, position in that check's mlist).
+    g.col_ptr.resize(N + 1);
+    g.col_deg.resize(N);
+    g.col_refs.resize(g.E);
+    int e = 0;
+    for (int i = 0; i < N; ++i) {
+        g.col_ptr[i] = e;
+        g.col_deg[i] = (uint8_t)num_nlist[i];
+        for (int k = 0; k < num_nlist[i]; ++k) {
+            const int j = nlist[i][k] - 1;
+            if (j < 0 || j >= M) return fmt("bit %ld lists check %ld (out of 1..M)", i, j + 1);
+            auto it = pos[j].find(i);
+            if (it == pos[j].end())
+                return fmt("bit %ld lists check %ld but that check does not list the bit", i, j + 1);
+            if (it->second < 0) return fmt("bit %ld lists check %ld twice", i, j + 1);
+            g.col_refs[e++] = ((uint32_t)j << kRefShift) | (uint32_t)it->second;
+            it->second = -1 - it->second;   // mark used (detect duplicates)
+        }
+    }
+    g.col_ptr[N] = e;
+    return "";
+}
+
+std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, RowSchedule &s)
+{
+    if (threads % 64 || threads < g.M) return "rows exceed threads";
+    if ((long)threads * cpt < g.N) return "bits exceed slots";
+    if (g.maxdc > dc) return "row degree exceeds kernel bound";
+    if (g.N > 65535) return "N exceeds 16-bit schedule";
+    s = RowSchedule();
+    s.threads = threads;
+    s.cpt = cpt;
+    s.dc = dc;
+    // Stable sort of columns by decreasing degree -> slot order.
+    std::vector<int> order(g.N);
+    for (int i = 0; i < g.N; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return g.col_deg[a] > g.col_deg[b]; });
+    const int nslots = threads * cpt;
+    const int ngroups = nslots / 64;
+    std::vector<int> gbase(ngroups + 1, 0);
+    for (int grp = 0; grp < ngroups; ++grp) {
+        int md = 0;
+        for (int l = 0; l < 64; ++l) {
+            const int slot = grp * 64 + l;
+            if (slot < g.N) md = std::max(md, (int)g.col_deg[order[slot]]);
+        }
+        gbase[grp + 1] = gbase[grp] + 64 * md;
+    }
+    s.e_pad = gbase[ngroups];
+    if (s.e_pad > 65535) return "padded edge count exceeds 16-bit schedule";
+    if (s.e_pad < g.N) s.e_pad = g.N;   // the c2v area doubles as channel staging
+    s.vn_col.assign(nslots, 0xffff);
+    s.vn_info.assign(nslots, 0);
+    s.cn_cols.assign((size_t)threads * dc, 0);
+    s.cn_pos.assign((size_t)threads * dc, 0);
+    s.cn_deg.assign(threads, 0);
+    for (int j = 0; j < g.M; ++j) {
+        s.cn_deg[j] = g.row_deg[j];
+        for (int k = 0; k < g.row_deg[j]; ++k)
+            s.cn_cols[(size_t)j * dc + k] = (uint16_t)g.row_cols[(size_t)j * std::max(g.maxdc, 1) + k];
+    }
+    // slot s = t + threads*i  <->  thread t, slot index i
+    for (int slot = 0; slot < g.N; ++slot) {
+        const int v = order[slot];
+        const int grp = slot >> 6, lane = slot & 63;
+        const int t = slot % threads, i = slot / threads;
+        const int idx = t * cpt + i;   // stored thread-major so a thread's slots are contiguous
+        s.vn_col[idx] = (uint16_t)v;
+        s.vn_info[idx] = (uint32_t)gbase[grp] | ((uint32_t)g.col_deg[v] << 16);
+        for (int kc = 0; kc < g.col_deg[v]; ++kc) {
+            const uint32_t ref = g.col_refs[g.col_ptr[v] + kc];
+            const int j = (int)(ref >> kRefShift), kr = (int)(ref & ((1u << kRefShift) - 1));
+            s.cn_pos[(size_t)j * dc + kr] = (uint16_t)(gbase[grp] + kc * 64 + lane);
+        }
+    }
+    return "";
+}
+
+std::string load_alist(const char *path, ldpc_graph &g)
+{
+    std::unique_ptr<FILE, int (*)(FILE *)> f(std::fopen(path, "r"), std::fclose);
+    if (!f) return std::string("cannot open alist file: ") + (path ? path : "(null)");
+    auto rd = [&](std::vector<int> &v, long n) -> bool {
+        v.resize(n);
+        for (long t = 0; t < n; ++t)
+            if (std::fscanf(f.get(), "%d ", &v[t]) != 1) return false;
+        return true;
+    };
+    std::vector<int> hdr, wn, wm, nl, ml;
+    if (!rd(hdr, 4)) return std::string("truncated alist header: ") + path;
+    const int N = hdr[0], M = hdr[1], mdv = hdr[2], mdc = hdr[3];
+    if (N <= 0 || M <= 0 || mdv < 0 || mdc < 0) return std::string("bad alist header: ") + path;
+    if (!rd(wn, N) || !rd(wm, M) || !rd(nl, (long)N * mdv) || !rd(ml, (long)M * mdc))
+        return std::string("truncated alist body (fixed-width reader): ") + path;
+    std::vector<const int *> np(N), mp(M);
+    for (int i = 0; i < N; ++i) {
+        if (wn[i] > mdv) return fmt("bit %ld weight %ld exceeds maxdv %ld", i, wn[i], mdv);
+        np[i] = nl.data() + (size_t)i * mdv;
+    }
+    for (int j = 0; j < M; ++j) {
+        if (wm[j] > mdc) return fmt("check %ld weight %ld exceeds maxdc %ld", j, wm[j], mdc);
+        mp[j] = ml.data() + (size_t)j * mdc;
+    }
+    std::string err = build_graph(N, M, wn.data(), np.data(), wm.data(), mp.data(), g);
+    if (!err.empty()) return err + " (" + path + ")";
+    return "";
+}
+
+}  // namespace ldpc

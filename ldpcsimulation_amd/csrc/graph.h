@@ -1,0 +1,57 @@
+// graph.h -- host-side Tanner-graph compiler (internal to libldpc_hip.so).
+//
+// Replaces the reference's alist_struct + find() edge search
+// (C_implementations/inc/alist.h:21-36, src/decodeMinSum.cpp:527-536) with
+// flat arrays the kernels index directly:
+//   row_cols[j*maxdc + k]  0-based bit index of the k-th edge of check j, in
+//                          mlist order (pads = 0, bounded by row_deg[j]);
+//   col_ptr[i]..col_ptr[i+1]  edges of bit i in nlist order (the order the
+//                          reference sums c2v in symNodeUpdates, :456-463);
+//   col_refs[e] = (j << 6) | k  the check j and the position k of bit i in
+//                          mlist[j] -- what find(mlist[j], ., i) returns.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+struct ldpc_graph {
+    int N = 0, M = 0, E = 0, maxdv = 0, maxdc = 0;
+    std::vector<int32_t> row_cols;   // [M * maxdc]
+    std::vector<uint8_t> row_deg;    // [M]
+    std::vector<int32_t> col_ptr;    // [N + 1]
+    std::vector<uint32_t> col_refs;  // [E]
+    std::vector<uint8_t> col_deg;    // [N]
+};
+
+namespace ldpc {
+constexpr int kMaxRowDegree = 58;   // sign bits that fit the packed row state
+constexpr int kRefShift = 6;
+
+// Static work schedule of the row-parallel kernel (kernels.hip, k_decode_rows):
+// one thread per check row (thread t = row t) and CPT bit-node slots per
+// thread (slot s = t + threads*i). Slots are the columns sorted by degree
+// (stable), so each 64-slot wave group has a near-uniform degree; the c2v
+// message of bit-node slot s, edge kc (nlist order) lives at element
+//   gbase[s >> 6] + kc*64 + (s & 63)
+// of the per-codeword c2v array (e_pad elements), so a wave's bit-node reads
+// are 64 consecutive words (conflict-free LDS).
+struct RowSchedule {
+    int threads = 0, cpt = 0, dc = 0, e_pad = 0;
+    std::vector<uint16_t> cn_cols;   // [threads * dc]  bit index of row edge k
+    std::vector<uint16_t> cn_pos;    // [threads * dc]  c2v element of row edge k
+    std::vector<uint8_t> cn_deg;     // [threads]
+    std::vector<uint16_t> vn_col;    // [threads * cpt] column of slot s (0xffff = none)
+    std::vector<uint32_t> vn_info;   // [threads * cpt] gbase | deg << 16
+};
+
+// Build from alist_struct-style arrays (1-based). Returns "" on success or
+// an error message.
+std::string build_graph(int N, int M, const int *num_nlist, const int *const *nlist,
+                        const int *num_mlist, const int *const *mlist, ldpc_graph &g);
+// Reference loadFile() semantics (src/alist.cpp:70-93, fixed-width lines).
+std::string load_alist(const char *path, ldpc_graph &g);
+// Row schedule for `threads` threads (multiple of 64, >= M), `cpt` bit slots
+// per thread (threads*cpt >= N) and row-degree bound dc. Returns "" or why the
+// graph does not fit (the caller then uses the generic kernel).
+std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, RowSchedule &s);
+}  // namespace ldpc

@@ -1,0 +1,69 @@
+// kernels.h -- internal launch interface between api.cpp and kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace ldpc {
+
+struct DevGraph {
+    int N, M, dcs;                  // dcs = row stride of row_cols (max(maxdc,1))
+    const int32_t *row_cols;        // [M * dcs]
+    const uint8_t *row_deg;         // [M]
+    const int32_t *col_ptr;         // [N + 1]
+    const uint32_t *col_refs;       // [E]  (check << 6) | position
+};
+
+enum { SRC_GIVEN = 0, SRC_PHILOX = 1 };
+
+struct DecodeArgs {
+    int batch, T, variant, quantize, saturate;
+    double ymax, nq, alpha, delta;
+    int src;
+    const void *y;                  // SRC_GIVEN: [batch][N] float|double (device)
+    const int8_t *c;                // SRC_GIVEN: [batch][N] bipolar, or null (+1)
+    const int8_t *cw_table;         // SRC_PHILOX: [cw_rows][N] bipolar, or null
+    int cw_rows;
+    uint64_t seed, first_cw;
+    uint32_t stream_id;
+    double sigma;
+    int8_t *d_out;                  // [batch][N] or null
+    void *y_out;                    // SRC_PHILOX: channel samples [batch][N] F (pre front-end) or null
+    int4 *frame_res;                // [batch] {bit_err, uncoded, syndrome_fail, 0} or null
+    unsigned long long *counts;     // [6] accumulated
+    unsigned long long *hist;       // [N] accumulated (weight w -> hist[w-1])
+};
+
+// Device copy of graph.h's RowSchedule (row-parallel kernel).
+struct RowSched {
+    int threads, cpt, dc, e_pad;
+    const uint16_t *cn_cols;        // [threads * dc]
+    const uint16_t *cn_pos;         // [threads * dc]
+    const uint8_t *cn_deg;          // [threads]
+    const uint16_t *vn_col;         // [threads * cpt]
+    const uint32_t *vn_info;        // [threads * cpt]
+};
+
+struct KernelChoice {
+    const char *name;               // "rows", "lds" or "global"
+    int lds_bytes;                  // dynamic LDS per block
+    size_t scratch_per_block;       // global kernel
+    int threads;
+    int cw_per_block;               // rows kernel: codewords decoded together per block
+};
+
+// Pick the kernel for a graph / precision. rs (may be null) is the row
+// schedule when the graph admits one; force selects "lds"/"global" for tests.
+KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force = nullptr);
+// Launch the decode. gscratch must hold choice.scratch_per_block * grid bytes
+// for the global kernel (grid returned through *grid_out, may be null).
+hipError_t launch_decode(const DevGraph &g, const DecodeArgs &a, bool f64, const KernelChoice &kc,
+                         void *gscratch, int gscratch_blocks, hipStream_t s, const RowSched *rs = nullptr,
+                         int num_cus = 256);
+int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc);
+
+// Row-kernel template bounds (host picks the smallest that fits).
+constexpr int kRowsMaxThreads = 1024;
+constexpr int kRowsCpt[] = {2, 4};
+constexpr int kRowsDc[] = {8, 16, 32};
+
+}  // namespace ldpc

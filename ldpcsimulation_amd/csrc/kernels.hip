@@ -1,0 +1,682 @@
+// kernels.hip -- CDNA4 (gfx950) kernels of the flooding min-sum decoder.
+//
+// One workgroup (4 waves) decodes one codeword for all T iterations with its
+// whole message state on chip:
+//   app[N]   posterior sums  sum = yq + sum_k c2v  (symNodeUpdates :456-463)
+//   yq[N]    channel samples after the front-end (:214-229)
+//   rows[M]  compressed check state {m1, m2, meta}: the two smallest |v2c|
+//            after normalisation/offset, argmin position and the sign of
+//            every c2v on the row (checkNodeUpdates :410-450 +
+//            applyNormalization :494-499 / applyOffset :503-515).
+// Every c2v message is a pure function of its row state, so the flooding
+// schedule needs no E-sized message arrays: the check phase rebuilds the old
+// c2v from the row state it owns and forms v2c = app - c2v_old, which is
+// bit-identical to the reference's v2c = sum - c2v (:469) because both are
+// the same IEEE subtraction of the same operands. The bit phase re-sums
+// yq + c2v in the reference's nlist order, so app (and the hard decision
+// d = sum > 0 ? +1 : -1, :471-474) is bit-identical too, in fp64 to the
+// reference and in fp32 to the fp32 restatement.
+//
+// The translation unit is compiled with -ffp-contract=off (see Makefile):
+// no FMA may fuse the channel's 1 + sigma*n or the quantiser.
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace ldpc {
+
+enum { V_MS = 0, V_NMS = 1, V_OMS = 2 };
+
+template <typename F> struct RowState;
+template <> struct __attribute__((aligned(16))) RowState<float> { float m1, m2; uint64_t meta; };
+template <> struct __attribute__((aligned(16))) RowState<double> { double m1, m2; uint64_t meta, pad; };
+
+template <typename F> __device__ __forceinline__ F dinf();
+template <> __device__ __forceinline__ float dinf<float>() { return __builtin_huge_valf(); }
+template <> __device__ __forceinline__ double dinf<double>() { return __builtin_huge_val(); }
+__device__ __forceinline__ float dabs(float x) { return __builtin_fabsf(x); }
+__device__ __forceinline__ double dabs(double x) { return __builtin_fabs(x); }
+__device__ __forceinline__ float dfloor(float x) { return __builtin_floorf(x); }
+__device__ __forceinline__ double dfloor(double x) { return __builtin_floor(x); }
+
+// sgn() of the reference (:518-523): x >= 0 -> +1 (so -0.0 -> +1, NaN -> -1).
+template <typename F> __device__ __forceinline__ F dsgn(F x) { return x >= F(0) ? F(1) : F(-1); }
+
+// quantize() (:480-489), same operation order.
+template <typename F>
+__device__ __forceinline__ F quantize(F x, F ymax, F nq)
+{
+    if (dabs(x) > ymax) return dsgn(x) * ymax;
+    F q = dsgn(x) * (dfloor(dabs(x) * (nq - F(1)) / (F(2) * ymax)) + F(0)) * (F(2) * ymax / (nq - F(1)));
+    if (q == F(0)) q = dsgn(x) * F(2) * ymax / (nq - F(1));
+    return q;
+}
+
+template <typename F>
+__device__ __forceinline__ F front_end(F y, const DecodeArgs &a)
+{
+    F q = y;
+    if (a.quantize) q = quantize<F>(y, (F)a.ymax, (F)a.nq);
+    if (a.saturate) {
+        const F ym = (F)a.ymax;
+        if (q > ym) q = ym;
+        if (q < -ym) q = -ym;
+    }
+    return q;
+}
+
+// ---------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. SC'11) + Box-Muller: 4 normals per call.
+// ---------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                              uint32_t k0, uint32_t k1, uint32_t out[4])
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+// Uniforms in (0,1): (u + 1/2) * 2^-32.
+__device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, float &n0, float &n1)
+{
+    const float a = (float)ua * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
+    const float r = (float)ur * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
+    const float rad = sqrtf(-2.0f * logf(r));
+    float s, c;
+    sincospif(2.0f * a, &s, &c);
+    n0 = rad * c;
+    n1 = rad * s;
+}
+__device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, double &n0, double &n1)
+{
+    const double a = ((double)ua + 0.5) * 2.3283064365386963e-10;
+    const double r = ((double)ur + 0.5) * 2.3283064365386963e-10;
+    const double rad = sqrt(-2.0 * log(r));
+    double s, c;
+    sincospi(2.0 * a, &s, &c);
+    n0 = rad * c;
+    n1 = rad * s;
+}
+
+// Sum over the workgroup (64-wide waves, <= 16 waves).
+__device__ __forceinline__ int block_sum(int x, int *red)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = x;
+    __syncthreads();
+    int s = 0;
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int i = 0; i < nw; ++i) s += red[i];
+    return s;
+}
+
+// ---------------------------------------------------------------------
+// One codeword, all T iterations. rows/app/yq may live in LDS or in a
+// per-workgroup global scratch slot; red is LDS.
+// ---------------------------------------------------------------------
+template <typename F, int SRC>
+__device__ __forceinline__ void decode_codeword(const DecodeArgs &a, const DevGraph &g, int b,
+                                                RowState<F> *rows, F *app, F *yq, int *red)
+{
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int N = g.N, M = g.M;
+    const uint64_t cw = a.first_cw + (uint64_t)b;
+
+    // ---- channel + front-end (:214-238) ----
+    const int8_t *cvec = nullptr;
+    if (SRC == SRC_GIVEN) {
+        if (a.c) cvec = a.c + (size_t)b * N;
+    } else if (a.cw_table) {
+        cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+    }
+    int unc = 0;
+    if (SRC == SRC_GIVEN) {
+        const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
+        for (int v = tid; v < N; v += nt) {
+            const F q = front_end<F>(y[v], a);
+            yq[v] = q;
+            app[v] = q;
+            const int cv = cvec ? cvec[v] : 1;
+            unc += ((q > F(0) ? 1 : -1) * cv < 0);
+        }
+    } else {
+        const F sigma = (F)a.sigma;
+        const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+        for (int g4 = tid; g4 * 4 < N; g4 += nt) {
+            uint32_t u[4];
+            philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+            F n[4];
+            box_muller(u[0], u[1], n[0], n[1]);
+            box_muller(u[2], u[3], n[2], n[3]);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int v = g4 * 4 + q4;
+                if (v < N) {
+                    const int cv = cvec ? cvec[v] : 1;
+                    const F yv = (F)cv * (F(1) + sigma * n[q4]);
+                    if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
+                    const F q = front_end<F>(yv, a);
+                    yq[v] = q;
+                    app[v] = q;
+                    unc += ((q > F(0) ? 1 : -1) * cv < 0);
+                }
+            }
+        }
+    }
+    for (int j = tid; j < M; j += nt) {
+        RowState<F> z;
+        z.m1 = F(0); z.m2 = F(0); z.meta = 0;
+        rows[j] = z;   // c2v_old = +0: v2c = yq on the first pass (:364-370)
+    }
+    __syncthreads();
+
+    const F alpha = (F)a.alpha, delta = (F)a.delta;
+    for (int it = 0; it < a.T; ++it) {
+        // ---- check nodes ----
+        for (int j = tid; j < M; j += nt) {
+            RowState<F> st = rows[j];
+            const int deg = g.row_deg[j];
+            const int32_t *rc = g.row_cols + (size_t)j * g.dcs;
+            const int oidx = (int)(st.meta & 63u);
+            const uint64_t osg = st.meta >> 6;
+            F mn1 = dinf<F>(), mn2 = dinf<F>();
+            int amin = 63;
+            uint64_t sg = 0;
+            for (int k = 0; k < deg; ++k) {
+                F cold = (k == oidx) ? st.m2 : st.m1;
+                if ((osg >> k) & 1u) cold = -cold;
+                const F x = app[rc[k]] - cold;               // v2c (:469)
+                sg |= (uint64_t)(!(x >= F(0))) << k;          // sgn(v2c) < 0
+                const F ax = dabs(x);
+                if (ax <= mn1) { mn2 = mn1; mn1 = ax; amin = k; }   // :428-433
+                else if (ax < mn2) { mn2 = ax; }                    // :434-437
+            }
+            const uint64_t degmask = (deg >= 64) ? ~0ull : ((1ull << deg) - 1ull);
+            uint64_t eff = (__popcll(sg) & 1) ? (sg ^ degmask) : sg;   // prod * sgn(v2c_k)
+            F M1 = mn1, M2 = mn2;
+            if (a.variant == V_NMS) {
+                M1 = mn1 / alpha;                              // :498 (IEEE division)
+                M2 = mn2 / alpha;
+            } else if (a.variant == V_OMS) {
+                const F t1 = mn1 - delta, t2 = mn2 - delta;    // :509
+                const bool p1 = t1 > F(0), p2 = t2 > F(0);
+                M1 = p1 ? t1 : F(0);
+                M2 = p2 ? t2 : F(0);
+                // sgn(c2v) of :511 maps -0.0 to +1; a zeroed message is +0 (:513)
+                const uint64_t abit = (amin < 64) ? (1ull << amin) : 0ull;
+                if (!p1 || mn1 == F(0)) eff &= abit;
+                if (!p2 || mn2 == F(0)) eff &= ~abit;
+            }
+            st.m1 = M1;
+            st.m2 = M2;
+            st.meta = (uint64_t)amin | (eff << 6);
+            rows[j] = st;
+        }
+        __syncthreads();
+        // ---- bit nodes: sum = yq + c2v in nlist order (:456-463) ----
+        for (int v = tid; v < N; v += nt) {
+            F sum = yq[v];
+            const int e1 = g.col_ptr[v + 1];
+            for (int e = g.col_ptr[v]; e < e1; ++e) {
+                const uint32_t ref = g.col_refs[e];
+                const int k = (int)(ref & 63u);
+                const RowState<F> st = rows[ref >> 6];
+                const F mag = (k == (int)(st.meta & 63u)) ? st.m2 : st.m1;
+                sum += ((st.meta >> (6 + k)) & 1u) ? -mag : mag;
+            }
+            app[v] = sum;
+        }
+        __syncthreads();
+    }
+
+    // ---- decisions, error weight (:270, :382-393), syndrome ----
+    int w = 0;
+    for (int v = tid; v < N; v += nt) {
+        const int d = app[v] > F(0) ? 1 : -1;                 // :471-474
+        const int cv = cvec ? cvec[v] : 1;
+        w += (d != cv);
+        if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+    }
+    int synd = 0;
+    for (int j = tid; j < M; j += nt) {
+        const int deg = g.row_deg[j];
+        const int32_t *rc = g.row_cols + (size_t)j * g.dcs;
+        int par = 0;
+        for (int k = 0; k < deg; ++k) par ^= (app[rc[k]] > F(0)) ? 0 : 1;
+        synd |= par;
+    }
+    w = block_sum(w, red);
+    unc = block_sum(unc, red);
+    synd = block_sum(synd, red);
+    if (tid == 0) {
+        atomicAdd(&a.counts[0], (unsigned long long)w);
+        atomicAdd(&a.counts[1], (unsigned long long)(w > 0));
+        atomicAdd(&a.counts[2], (unsigned long long)unc);
+        atomicAdd(&a.counts[3], 1ull);
+        atomicAdd(&a.counts[4], (unsigned long long)a.T);
+        atomicAdd(&a.counts[5], (unsigned long long)(synd > 0));
+        if (w > 0 && a.hist) atomicAdd(&a.hist[w - 1], 1ull);
+        if (a.frame_res) a.frame_res[b] = make_int4(w, unc, synd > 0 ? 1 : 0, 0);
+    }
+    __syncthreads();
+}
+
+// State in LDS: one codeword per workgroup, grid = batch.
+template <typename F, int SRC>
+__global__ __launch_bounds__(256) void k_decode_lds(DecodeArgs a, DevGraph g)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    RowState<F> *rows = reinterpret_cast<RowState<F> *>(smem);
+    F *app = reinterpret_cast<F *>(smem + sizeof(RowState<F>) * (size_t)g.M);
+    F *yq = app + g.N;
+    int *red = reinterpret_cast<int *>(yq + g.N);
+    decode_codeword<F, SRC>(a, g, blockIdx.x, rows, app, yq, red);
+}
+
+// State in a global scratch slot per workgroup (codes whose state exceeds
+// LDS, e.g. DVB-S2 N=64800): persistent grid, codewords strided.
+template <typename F, int SRC>
+__global__ __launch_bounds__(256) void k_decode_global(DecodeArgs a, DevGraph g, unsigned char *scratch,
+                                                       size_t slot_bytes)
+{
+    __shared__ int red[16];
+    unsigned char *base = scratch + slot_bytes * blockIdx.x;
+    RowState<F> *rows = reinterpret_cast<RowState<F> *>(base);
+    F *app = reinterpret_cast<F *>(base + sizeof(RowState<F>) * (size_t)g.M);
+    F *yq = app + g.N;
+    for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
+        decode_codeword<F, SRC>(a, g, b, rows, app, yq, red);
+}
+
+// =====================================================================
+// Row-parallel kernel (the throughput path).
+//
+// Block = `threads` threads (>= M, multiple of 64): thread t owns check row t
+// for the whole persistent launch, with its row's bit indices and c2v slot
+// positions held in registers (loaded once per launch from the RowSchedule
+// built on the host), and CPT bit-node slots (columns sorted by degree).
+// Each thread decodes C codewords at once (independent instruction streams).
+// LDS per codeword: app[N] + c2v[e_pad], c2v in wave-slot-major order so the
+// bit-node phase reads 64 consecutive words per wave instruction.
+// Per iteration: check phase (gather app, rebuild the old c2v from the row
+// state kept in registers, v2c = app - c2v_old, min/second-min/argmin/signs,
+// normalise/offset, scatter the new c2v) | barrier | bit phase (sum yq + c2v
+// in nlist order, write app) | barrier.
+// =====================================================================
+template <int DC> struct MetaOf { using T = uint32_t; static constexpr int SH = 5; };
+template <> struct MetaOf<32> { using T = uint64_t; static constexpr int SH = 6; };
+
+template <int DC>
+__device__ __forceinline__ int u16_at(const uint32_t (&w)[DC / 2], int k)
+{
+    return (int)((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
+}
+
+template <typename F, int SRC, int C, int DC, int CPT>
+__global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, RowSched rs)
+{
+    using MT = typename MetaOf<DC>::T;
+    constexpr int SH = MetaOf<DC>::SH;
+    constexpr MT NONE = (MT)((1u << SH) - 1u);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
+    const int N = g.N, EP = rs.e_pad;
+    F *app = reinterpret_cast<F *>(smem);        // [C][N]
+    F *c2v = app + C * N;                         // [C][EP]
+    int *red = reinterpret_cast<int *>(c2v + C * EP);
+
+    // ---- the thread's share of the graph, in registers for the whole launch ----
+    const int deg = rs.cn_deg[tid];
+    uint32_t colw[DC / 2], posw[DC / 2];
+#pragma unroll
+    for (int q = 0; q < DC / 8; ++q) {
+        const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)tid * DC)[q];
+        const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)tid * DC)[q];
+        colw[4 * q + 0] = xc.x; colw[4 * q + 1] = xc.y; colw[4 * q + 2] = xc.z; colw[4 * q + 3] = xc.w;
+        posw[4 * q + 0] = xp.x; posw[4 * q + 1] = xp.y; posw[4 * q + 2] = xp.z; posw[4 * q + 3] = xp.w;
+    }
+    int vcol[CPT];
+    uint32_t vinfo[CPT];
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = rs.vn_col[tid * CPT + i];
+        vcol[i] = c == 0xffff ? -1 : c;
+        vinfo[i] = rs.vn_info[tid * CPT + i];
+    }
+
+    const F alpha = (F)a.alpha, delta = (F)a.delta;
+    const int ngrp = (a.batch + C - 1) / C;
+    for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+        // ---- channel (:214-238), staged through the c2v area ----
+        int unc[C];
+        const int8_t *cvec[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            unc[c] = 0;
+            cvec[c] = nullptr;
+            const int b = grp * C + c;
+            if (b >= a.batch) continue;
+            const uint64_t cw = a.first_cw + (uint64_t)b;
+            F *stage = c2v + c * EP;
+            if (SRC == SRC_GIVEN) {
+                if (a.c) cvec[c] = a.c + (size_t)b * N;
+                const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
+                for (int v = tid; v < N; v += nt) {
+                    const F q = front_end<F>(y[v], a);
+                    stage[v] = q;
+                    const int cv = cvec[c] ? cvec[c][v] : 1;
+                    unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
+                }
+            } else {
+                if (a.cw_table) cvec[c] = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+                const F sigma = (F)a.sigma;
+                const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+                for (int g4 = tid; g4 * 4 < N; g4 += nt) {
+                    uint32_t u[4];
+                    philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                    F n[4];
+                    box_muller(u[0], u[1], n[0], n[1]);
+                    box_muller(u[2], u[3], n[2], n[3]);
+#pragma unroll
+                    for (int q4 = 0; q4 < 4; ++q4) {
+                        const int v = g4 * 4 + q4;
+                        if (v < N) {
+                            const int cv = cvec[c] ? cvec[c][v] : 1;
+                            const F yv = (F)cv * (F(1) + sigma * n[q4]);
+                            if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
+                            const F q = front_end<F>(yv, a);
+                            stage[v] = q;
+                            unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        F yq[C][CPT];
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int v = vcol[i];
+                yq[c][i] = v >= 0 ? c2v[c * EP + v] : F(0);
+                if (v >= 0) app[c * N + v] = yq[c][i];   // v2c = yq on the first pass (:364-370)
+            }
+        __syncthreads();
+
+        F m1[C], m2[C];
+        MT meta[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) { m1[c] = F(0); m2[c] = F(0); meta[c] = 0; }   // c2v_old = +0
+
+        for (int it = 0; it < a.T; ++it) {
+            // ---- check nodes (:410-450, :494-515) ----
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const F *appc = app + c * N;
+                const int oidx = (int)(meta[c] & NONE);
+                F mn1 = dinf<F>(), mn2 = dinf<F>();
+                MT amin = NONE, sg = 0;
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    if (k < deg) {
+                        const F mo = (k == oidx) ? m2[c] : m1[c];
+                        const F cold = ((meta[c] >> (SH + k)) & 1u) ? -mo : mo;
+                        const F x = appc[u16_at<DC>(colw, k)] - cold;        // v2c (:469)
+                        sg |= (MT)(!(x >= F(0))) << k;                        // sgn(v2c) (:518-523)
+                        const F ax = dabs(x);
+                        const bool le = ax <= mn1;                            // :428
+                        mn2 = le ? mn1 : ((ax < mn2) ? ax : mn2);             // :430, :434-437
+                        mn1 = le ? ax : mn1;
+                        amin = le ? (MT)k : amin;
+                    }
+                }
+                const MT degmask = (deg >= (int)(8 * sizeof(MT))) ? ~(MT)0 : (((MT)1 << deg) - 1);
+                MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask) : sg;
+                F M1 = mn1, M2 = mn2;
+                if (a.variant == V_NMS) {
+                    M1 = mn1 / alpha;
+                    M2 = mn2 / alpha;
+                } else if (a.variant == V_OMS) {
+                    const F t1 = mn1 - delta, t2 = mn2 - delta;
+                    const bool p1 = t1 > F(0), p2 = t2 > F(0);
+                    M1 = p1 ? t1 : F(0);
+                    M2 = p2 ? t2 : F(0);
+                    const MT abit = (amin < (MT)DC) ? ((MT)1 << amin) : (MT)0;
+                    if (!p1 || mn1 == F(0)) eff &= abit;
+                    if (!p2 || mn2 == F(0)) eff &= ~abit;
+                }
+                F *c2vc = c2v + c * EP;
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    if (k < deg) {
+                        const F mag = ((MT)k == amin) ? M2 : M1;
+                        c2vc[u16_at<DC>(posw, k)] = ((eff >> k) & 1u) ? -mag : mag;
+                    }
+                }
+                m1[c] = M1;
+                m2[c] = M2;
+                meta[c] = amin | (eff << SH);
+            }
+            __syncthreads();
+            // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int v = vcol[i];
+                if (v >= 0) {
+                    const int gb = (int)(vinfo[i] & 0xffffu) + lane, dg = (int)(vinfo[i] >> 16);
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        const F *cc = c2v + c * EP + gb;
+                        F sum = yq[c][i];
+                        for (int k = 0; k < dg; ++k) sum += cc[k * 64];
+                        app[c * N + v] = sum;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+
+        // ---- decisions, error weight, syndrome, accounting ----
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int b = grp * C + c;
+            const bool valid = b < a.batch;
+            int w = 0, synd = 0;
+            if (valid) {
+#pragma unroll
+                for (int i = 0; i < CPT; ++i) {
+                    const int v = vcol[i];
+                    if (v >= 0) {
+                        const int d = app[c * N + v] > F(0) ? 1 : -1;
+                        const int cv = cvec[c] ? cvec[c][v] : 1;
+                        w += (d != cv);
+                        if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+                    }
+                }
+                int par = 0;
+#pragma unroll
+                for (int k = 0; k < DC; ++k)
+                    if (k < deg) par ^= (app[c * N + u16_at<DC>(colw, k)] > F(0)) ? 0 : 1;
+                synd = par;
+            }
+            w = block_sum(w, red);
+            const int uc = block_sum(unc[c], red);
+            synd = block_sum(synd, red);
+            if (tid == 0 && valid) {
+                atomicAdd(&a.counts[0], (unsigned long long)w);
+                atomicAdd(&a.counts[1], (unsigned long long)(w > 0));
+                atomicAdd(&a.counts[2], (unsigned long long)uc);
+                atomicAdd(&a.counts[3], 1ull);
+                atomicAdd(&a.counts[4], (unsigned long long)a.T);
+                atomicAdd(&a.counts[5], (unsigned long long)(synd > 0));
+                if (w > 0 && a.hist) atomicAdd(&a.hist[w - 1], 1ull);
+                if (a.frame_res) a.frame_res[b] = make_int4(w, uc, synd > 0 ? 1 : 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+static size_t state_bytes(const DevGraph &g, bool f64)
+{
+    const size_t rs = f64 ? sizeof(RowState<double>) : sizeof(RowState<float>);
+    const size_t fs = f64 ? 8 : 4;
+    return rs * (size_t)g.M + 2 * fs * (size_t)g.N;
+}
+
+constexpr int kThreads = 256;
+constexpr size_t kMaxLds = 160 * 1024;
+
+// Codewords per thread: 2 for the fp32 DC=8 kernel (no spills at 101 VGPRs),
+// 1 where two would spill (fp64, wider rows).
+static int rows_cw_per_block(bool f64, int dc) { return (!f64 && dc == 8) ? 2 : 1; }
+
+static size_t rows_lds(const DevGraph &g, const RowSched &rs, bool f64, int C)
+{
+    const size_t fs = f64 ? 8 : 4;
+    return ((size_t)C * ((size_t)g.N + (size_t)rs.e_pad) * fs + 64 + 15) & ~(size_t)15;
+}
+
+KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force)
+{
+    KernelChoice kc;
+    kc.threads = kThreads;
+    kc.cw_per_block = 1;
+    kc.scratch_per_block = 0;
+    const bool want_lds = force && force[0] == 'l';
+    const bool want_global = force && force[0] == 'g';
+    if (rs && rs->threads > 0 && !want_lds && !want_global) {
+        const int C = rows_cw_per_block(f64, rs->dc);
+        const size_t lds = rows_lds(g, *rs, f64, C);
+        if (lds <= kMaxLds) {
+            kc.name = "rows";
+            kc.lds_bytes = (int)lds;
+            kc.threads = rs->threads;
+            kc.cw_per_block = C;
+            return kc;
+        }
+    }
+    const size_t lds = (state_bytes(g, f64) + 64 + 15) & ~(size_t)15;
+    if (lds <= kMaxLds && !want_global) {
+        kc.name = "lds";
+        kc.lds_bytes = (int)lds;
+    } else {
+        kc.name = "global";
+        kc.lds_bytes = 0;
+        kc.scratch_per_block = (state_bytes(g, f64) + 255) & ~(size_t)255;
+    }
+    return kc;
+}
+
+template <typename F, int SRC>
+static hipError_t launch_t(const DevGraph &g, const DecodeArgs &a, const KernelChoice &kc, void *gs,
+                           int gblocks, hipStream_t s)
+{
+    if (kc.lds_bytes > 0) {
+        auto fn = k_decode_lds<F, SRC>;
+        if (kc.lds_bytes > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               kc.lds_bytes);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(fn, dim3(a.batch), dim3(kc.threads), kc.lds_bytes, s, a, g);
+    } else {
+        const int grid = gblocks < a.batch ? gblocks : a.batch;
+        hipLaunchKernelGGL((k_decode_global<F, SRC>), dim3(grid), dim3(kc.threads), 0, s, a, g,
+                           (unsigned char *)gs, kc.scratch_per_block);
+    }
+    return hipGetLastError();
+}
+
+// Row kernel: dispatch on (C, DC, CPT). Persistent grid of the resident blocks.
+template <typename F, int SRC, int C, int DC, int CPT>
+static hipError_t launch_rows_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, const KernelChoice &kc,
+                                hipStream_t s, int num_cus)
+{
+    auto fn = k_decode_rows<F, SRC, C, DC, CPT>;
+    hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, kc.lds_bytes);
+    if (e != hipSuccess) return e;
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kc.threads, kc.lds_bytes);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    const int ngrp = (a.batch + C - 1) / C;
+    int grid = per_cu * num_cus;
+    if (grid > ngrp) grid = ngrp;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a, g, rs);
+    return hipGetLastError();
+}
+
+template <typename F, int SRC>
+static hipError_t launch_rows_dc(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, const KernelChoice &kc,
+                                 hipStream_t s, int num_cus)
+{
+    constexpr int C8 = sizeof(F) == 4 ? 2 : 1;
+#define LDPC_ROWS_CASE(CV, DCV, CPTV) \
+    if (rs.dc == DCV && rs.cpt == CPTV) return launch_rows_t<F, SRC, CV, DCV, CPTV>(g, rs, a, kc, s, num_cus);
+    LDPC_ROWS_CASE(C8, 8, 2)
+    LDPC_ROWS_CASE(C8, 8, 4)
+    LDPC_ROWS_CASE(1, 16, 2)
+    LDPC_ROWS_CASE(1, 16, 4)
+    LDPC_ROWS_CASE(1, 32, 2)
+    LDPC_ROWS_CASE(1, 32, 4)
+#undef LDPC_ROWS_CASE
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_decode(const DevGraph &g, const DecodeArgs &a, bool f64, const KernelChoice &kc,
+                         void *gscratch, int gscratch_blocks, hipStream_t s, const RowSched *rs, int num_cus)
+{
+    if (a.batch <= 0) return hipSuccess;
+    if (kc.name[0] == 'r') {
+        if (!rs) return hipErrorInvalidValue;
+        if (f64)
+            return a.src == SRC_GIVEN ? launch_rows_dc<double, SRC_GIVEN>(g, *rs, a, kc, s, num_cus)
+                                      : launch_rows_dc<double, SRC_PHILOX>(g, *rs, a, kc, s, num_cus);
+        return a.src == SRC_GIVEN ? launch_rows_dc<float, SRC_GIVEN>(g, *rs, a, kc, s, num_cus)
+                                  : launch_rows_dc<float, SRC_PHILOX>(g, *rs, a, kc, s, num_cus);
+    }
+    if (f64) {
+        return a.src == SRC_GIVEN ? launch_t<double, SRC_GIVEN>(g, a, kc, gscratch, gscratch_blocks, s)
+                                  : launch_t<double, SRC_PHILOX>(g, a, kc, gscratch, gscratch_blocks, s);
+    }
+    return a.src == SRC_GIVEN ? launch_t<float, SRC_GIVEN>(g, a, kc, gscratch, gscratch_blocks, s)
+                              : launch_t<float, SRC_PHILOX>(g, a, kc, gscratch, gscratch_blocks, s);
+}
+
+int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc)
+{
+    int nb = 0;
+    hipError_t e;
+    if (kc.name[0] == 'r') {
+        // the row kernels of one (C) share the LDS / thread shape
+        const void *fn = f64 ? (const void *)k_decode_rows<double, SRC_PHILOX, 1, 8, 2>
+                             : (kc.cw_per_block == 2 ? (const void *)k_decode_rows<float, SRC_PHILOX, 2, 8, 2>
+                                                     : (const void *)k_decode_rows<float, SRC_PHILOX, 1, 16, 2>);
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kc.lds_bytes);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads, kc.lds_bytes);
+    } else if (kc.lds_bytes > 0) {
+        const void *fn = f64 ? (const void *)k_decode_lds<double, SRC_PHILOX> : (const void *)k_decode_lds<float, SRC_PHILOX>;
+        (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kc.lds_bytes);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads, kc.lds_bytes);
+    } else {
+        e = f64 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_global<double, SRC_PHILOX>,
+                                                               kc.threads, 0)
+                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_global<float, SRC_PHILOX>,
+                                                               kc.threads, 0);
+    }
+    if (e != hipSuccess) { (void)hipGetLastError(); return 0; }
+    return nb;
+}
+
+}  // namespace ldpc

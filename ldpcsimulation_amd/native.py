@@ -1,0 +1,276 @@
+"""ctypes binding of the C ABI in include/ldpc_hip.h (libldpc_hip.so).
+
+This is the only way the Python side reaches the decoder: there is no CPU
+fallback. If the HIP library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "lib", "libldpc_hip.so")
+
+LDPC_OK = 0
+MS, NMS, OMS = 0, 1, 2
+F32, F64 = 0, 1
+_STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
+
+
+class LdpcError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ldpc error {code} ({_STATUS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Counts(C.Structure):
+    _fields_ = [("bit_err", C.c_int64), ("frame_err", C.c_int64), ("uncoded_bit_err", C.c_int64),
+                ("frames", C.c_int64), ("iters", C.c_int64), ("syndrome_fail", C.c_int64)]
+
+    def as_dict(self) -> dict:
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+    def as_array(self) -> np.ndarray:
+        return np.array([getattr(self, k) for k, _ in self._fields_], dtype=np.int64)
+
+
+FRAME_DTYPE = np.dtype([("bit_err", np.int32), ("uncoded_bit_err", np.int32),
+                        ("syndrome_fail", np.int32), ("reserved", np.int32)])
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("variant", C.c_int32), ("precision", C.c_int32), ("T", C.c_int32),
+                ("quantize", C.c_int32), ("saturate", C.c_int32), ("qbits", C.c_int32),
+                ("ymax", C.c_double), ("alpha", C.c_double), ("delta", C.c_double)]
+
+
+@dataclass
+class DecoderConfig:
+    """Runtime form of the reference's compile-time decoder switches."""
+    variant: int = MS            # MS | NMS (-D normalizedMS) | OMS (-D offsetMS)
+    T: int = 10                  # iterations (fixed, no early termination)
+    precision: int = F32         # F32 throughput path | F64 reference-exact path
+    alpha: float = 1.0           # NMS divisor
+    delta: float = 0.0           # OMS offset
+    quantize: bool = False       # -D quantizeSamples
+    saturate: bool = False       # -D saturateSamples
+    ymax: float = 0.0
+    qbits: int = 0
+
+    def _c(self) -> _Cfg:
+        return _Cfg(self.variant, self.precision, self.T, int(self.quantize), int(self.saturate),
+                    self.qbits, self.ymax, self.alpha, self.delta)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"HIP decoder library not built: {LIB_PATH} (run __graft_entry__.build() or `make`)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, u32, u64, dbl = C.c_void_p, C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
+    sig = {
+        "ldpc_abi_version": ([], i32),
+        "ldpc_last_error": ([], C.c_char_p),
+        "ldpc_graph_create": ([i32, i32, vp, vp, vp, vp, C.POINTER(vp)], i32),
+        "ldpc_graph_load_alist": ([C.c_char_p, C.POINTER(vp)], i32),
+        "ldpc_graph_info": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),
+                             C.POINTER(i32)], i32),
+        "ldpc_graph_destroy": ([vp], None),
+        "ldpc_device_count": ([C.POINTER(i32)], i32),
+        "ldpc_ctx_create": ([i32, vp, i32, C.POINTER(vp)], i32),
+        "ldpc_ctx_set_stream": ([vp, vp], i32),
+        "ldpc_ctx_synchronize": ([vp], i32),
+        "ldpc_ctx_destroy": ([vp], None),
+        "ldpc_decode_batch": ([vp, vp, i32, C.POINTER(_Cfg), vp, vp, vp, C.POINTER(Counts)], i32),
+        "ldpc_sim_set_codewords": ([vp, vp, i32], i32),
+        "ldpc_sim_launch": ([vp, dbl, dbl, C.POINTER(_Cfg), u64, u32, u64, i32, vp], i32),
+        "ldpc_ctx_read_counts": ([vp, C.POINTER(Counts), i32], i32),
+        "ldpc_ctx_read_histogram": ([vp, vp, i32], i32),
+        "ldpc_sim_batch": ([vp, dbl, dbl, C.POINTER(_Cfg), u64, u32, u64, i32, vp, C.POINTER(Counts)], i32),
+        "ldpc_sim_trace": ([vp, dbl, dbl, C.POINTER(_Cfg), u64, u32, u64, i32, vp, vp, vp, C.POINTER(Counts)],
+                           i32),
+        "ldpc_ctx_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i32),
+        "ldpc_ctx_kernel_info": ([vp, C.POINTER(_Cfg), C.c_char_p, i32, C.POINTER(i32), C.POINTER(i32)], i32),
+    }
+    for name, (argt, rest) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = argt
+        fn.restype = rest
+    _lib = L
+    return L
+
+
+# Every symbol include/ldpc_hip.h declares (checked by tests/test_abi.py).
+EXPORTED = ["ldpc_abi_version", "ldpc_last_error", "ldpc_graph_create", "ldpc_graph_load_alist",
+            "ldpc_graph_info", "ldpc_graph_destroy", "ldpc_device_count", "ldpc_ctx_create",
+            "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
+            "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",
+            "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info"]
+
+
+def _check(rc: int):
+    if rc != LDPC_OK:
+        raise LdpcError(rc, lib().ldpc_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = lib().ldpc_device_count(C.byref(n))
+    return n.value if rc == LDPC_OK else 0
+
+
+class Graph:
+    """Immutable Tanner graph (H matrix) on the host side of the ABI."""
+
+    def __init__(self, handle):
+        self._h = handle
+        N, M, E, dv, dc = (C.c_int() for _ in range(5))
+        _check(lib().ldpc_graph_info(self._h, C.byref(N), C.byref(M), C.byref(E), C.byref(dv), C.byref(dc)))
+        self.N, self.M, self.E, self.maxdv, self.maxdc = N.value, M.value, E.value, dv.value, dc.value
+
+    @classmethod
+    def from_alist(cls, path: str) -> "Graph":
+        h = C.c_void_p()
+        _check(lib().ldpc_graph_load_alist(os.fspath(path).encode(), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_lists(cls, N: int, M: int, nlist, mlist) -> "Graph":
+        """nlist[i]: 1-based checks of bit i; mlist[j]: 1-based bits of check j (alist_struct form)."""
+        num_n = (C.c_int * N)(*[len(x) for x in nlist])
+        num_m = (C.c_int * M)(*[len(x) for x in mlist])
+        keep = [(C.c_int * max(len(x), 1))(*x) for x in nlist] + [(C.c_int * max(len(x), 1))(*x) for x in mlist]
+        np_ = (C.c_void_p * N)(*[C.cast(a, C.c_void_p) for a in keep[:N]])
+        mp_ = (C.c_void_p * M)(*[C.cast(a, C.c_void_p) for a in keep[N:]])
+        h = C.c_void_p()
+        _check(lib().ldpc_graph_create(N, M, num_n, np_, num_m, mp_, C.byref(h)))
+        return cls(h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.ldpc_graph_destroy(h)
+            self._h = None
+
+
+def _ptr(a) -> Optional[int]:
+    """Address of a numpy array or a torch tensor (host or device)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return a.ctypes.data
+    if hasattr(a, "data_ptr"):
+        if not a.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return a.data_ptr()
+    raise TypeError(type(a))
+
+
+class Context:
+    """One device context (stream, counters, scratch) bound to a graph."""
+
+    def __init__(self, graph: Graph, device: int = 0, max_batch: int = 65536):
+        self.graph = graph
+        self.device = device
+        self.max_batch = max_batch
+        h = C.c_void_p()
+        _check(lib().ldpc_ctx_create(device, graph._h, max_batch, C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.ldpc_ctx_destroy(h)
+            self._h = None
+
+    def set_stream(self, stream_handle: Optional[int]):
+        _check(lib().ldpc_ctx_set_stream(self._h, stream_handle))
+
+    def synchronize(self):
+        _check(lib().ldpc_ctx_synchronize(self._h))
+
+    def decode(self, y, cfg: DecoderConfig, c=None, want_decisions: bool = True, want_frames: bool = True):
+        """Decode y[batch, N] (float32 for F32, float64 for F64; numpy or torch, host or device).
+
+        Returns (d [batch,N] int8 or None, frames structured array or None, Counts)."""
+        N = self.graph.N
+        if isinstance(y, np.ndarray):
+            want = np.float64 if cfg.precision == F64 else np.float32
+            if y.dtype != want:
+                raise TypeError(f"y must be {np.dtype(want)} for this precision, got {y.dtype}")
+            y = np.ascontiguousarray(y)
+            batch = y.size // N
+        else:
+            batch = y.numel() // N
+        if c is not None and isinstance(c, np.ndarray):
+            c = np.ascontiguousarray(c, dtype=np.int8)
+        d = np.empty((batch, N), dtype=np.int8) if want_decisions else None
+        fr = np.empty(batch, dtype=FRAME_DTYPE) if want_frames else None
+        cnt = Counts()
+        _check(lib().ldpc_decode_batch(self._h, _ptr(y), batch, C.byref(cfg._c()), _ptr(c), _ptr(d), _ptr(fr),
+                                       C.byref(cnt)))
+        return d, fr, cnt
+
+    def set_codewords(self, bits: Optional[np.ndarray]):
+        if bits is None:
+            _check(lib().ldpc_sim_set_codewords(self._h, None, 0))
+            return
+        bits = np.ascontiguousarray(bits, dtype=np.uint8).reshape(-1, self.graph.N)
+        _check(lib().ldpc_sim_set_codewords(self._h, bits.ctypes.data, bits.shape[0]))
+
+    def sim_launch(self, ebn0_db: float, R: float, cfg: DecoderConfig, seed: int, stream_id: int, first_cw: int,
+                   batch: int, frames_dev=None):
+        _check(lib().ldpc_sim_launch(self._h, ebn0_db, R, C.byref(cfg._c()), seed, stream_id, first_cw, batch,
+                                     _ptr(frames_dev)))
+
+    def sim_batch(self, ebn0_db: float, R: float, cfg: DecoderConfig, seed: int, stream_id: int, first_cw: int,
+                  batch: int, want_frames: bool = True):
+        fr = np.empty(batch, dtype=FRAME_DTYPE) if want_frames else None
+        cnt = Counts()
+        _check(lib().ldpc_sim_batch(self._h, ebn0_db, R, C.byref(cfg._c()), seed, stream_id, first_cw, batch,
+                                    _ptr(fr), C.byref(cnt)))
+        return fr, cnt
+
+    def sim_trace(self, ebn0_db: float, R: float, cfg: DecoderConfig, seed: int, stream_id: int, first_cw: int,
+                  batch: int):
+        """sim_batch that also returns the generated channel samples and decisions."""
+        N = self.graph.N
+        y = np.empty((batch, N), dtype=np.float64 if cfg.precision == F64 else np.float32)
+        d = np.empty((batch, N), dtype=np.int8)
+        fr = np.empty(batch, dtype=FRAME_DTYPE)
+        cnt = Counts()
+        _check(lib().ldpc_sim_trace(self._h, ebn0_db, R, C.byref(cfg._c()), seed, stream_id, first_cw, batch,
+                                    y.ctypes.data, d.ctypes.data, fr.ctypes.data, C.byref(cnt)))
+        return y, d, fr, cnt
+
+    def read_counts(self, reset: bool = False) -> Counts:
+        cnt = Counts()
+        _check(lib().ldpc_ctx_read_counts(self._h, C.byref(cnt), int(reset)))
+        return cnt
+
+    def read_histogram(self, reset: bool = False) -> np.ndarray:
+        h = np.zeros(self.graph.N, dtype=np.int64)
+        _check(lib().ldpc_ctx_read_histogram(self._h, h.ctypes.data, int(reset)))
+        return h
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        _check(lib().ldpc_ctx_last_kernel_ms(self._h, C.byref(ms)))
+        return float(ms.value)
+
+    def kernel_info(self, cfg: DecoderConfig) -> dict:
+        name = C.create_string_buffer(32)
+        lds, bpc = C.c_int(), C.c_int()
+        _check(lib().ldpc_ctx_kernel_info(self._h, C.byref(cfg._c()), name, 32, C.byref(lds), C.byref(bpc)))
+        return {"kernel": name.value.decode(), "lds_bytes": lds.value, "blocks_per_cu": bpc.value}

@@ -1,0 +1,184 @@
+"""Monte-Carlo SNR driver: the reference's per-SNR frame loop, batched and sharded.
+
+Reference: C_implementations/src/decodeMinSum.cpp:146-311 (one SNR point per
+process; frames until errors >= 200 AND wordErrors >= 40) and the sweep
+scripts (scripts/minsum_example_*.sh:23-27, one background process per SNR
+point appending one line each to a shared log).
+
+Here one SNR point is a sequence of rounds. In round k, rank r of W decodes
+the global frames [k*B*W + r*B, k*B*W + (r+1)*B) on its own GPU with
+counter-based noise keyed by the global frame index, so the frames -- and the
+statistics for a given total -- do not depend on W or B. After each round the
+six int64 counters are summed over ranks (one all-reduce of 48 bytes, RCCL
+over xGMI with the nccl backend, gloo on CPU). With exact_stop (default) the
+round that crosses the stop rule gathers its per-frame results and cuts at the
+exact frame where the sequential reference would have stopped, so the
+reported totals equal a frame-by-frame run of the same noise.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import numpy as np
+
+from .native import FRAME_DTYPE
+
+COUNT_KEYS = ("bit_err", "frame_err", "uncoded_bit_err", "frames", "iters", "syndrome_fail")
+
+
+@dataclass
+class PointResult:
+    ebn0_db: float
+    N: int
+    T: int
+    counts: dict = field(default_factory=dict)
+    rounds: int = 0
+    hist: Optional[np.ndarray] = None   # error_weight_hist (:173), exact-stop frames only
+
+    @property
+    def ber(self) -> float:
+        bits = self.counts["frames"] * self.N
+        return self.counts["bit_err"] / bits if bits else float("nan")
+
+    @property
+    def fer(self) -> float:
+        f = self.counts["frames"]
+        return self.counts["frame_err"] / f if f else float("nan")
+
+    @property
+    def avg_iters(self) -> float:
+        f = self.counts["frames"]
+        return self.counts["iters"] / f if f else float("nan")
+
+    def log_line(self, alist_name: str, extra=()) -> str:
+        """The reference's log line (:313-329): SNR BER avgIt FER T [Ymax] [alpha] [delta] alist."""
+        vals = [_cpp_double(self.ebn0_db), _cpp_double(self.ber), _cpp_double(self.avg_iters),
+                _cpp_double(self.fer), str(self.T)] + [_cpp_double(x) for x in extra] + [alist_name]
+        return "\t".join(vals)
+
+
+def _cpp_double(x: float) -> str:
+    """std::ostream default formatting of a double (%g, 6 significant digits)."""
+    return f"{x:g}"
+
+
+def stop_reached(bit_err: int, frame_err: int, min_bit_err: int = 200, min_frame_err: int = 40) -> bool:
+    """Negation of the loop condition (errors < 200 || wordErrors < 40) at :189."""
+    return not (bit_err < min_bit_err or frame_err < min_frame_err)
+
+
+def exact_cut(prev: np.ndarray, frames: np.ndarray, T: int, min_bit_err=200, min_frame_err=40):
+    """Apply the stop rule frame by frame. prev = counters before this round;
+    frames = this round's per-frame results in global frame order. Returns
+    (counters after the last frame the reference would decode, frames used)."""
+    acc = prev.copy()
+    used = 0
+    for w, unc, syn, _ in frames:
+        if stop_reached(acc[0], acc[1], min_bit_err, min_frame_err):
+            break
+        acc += (w, 1 if w > 0 else 0, unc, 1, T, syn)
+        used += 1
+    return acc, used
+
+
+class _Comm:
+    """Minimal collective layer: torch.distributed if initialised, else local."""
+
+    def __init__(self, device=None):
+        self.dist = None
+        self.rank, self.world = 0, 1
+        self.device = device
+        try:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                self.dist = dist
+                self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        except ImportError:
+            pass
+
+    def _tensor(self, arr: np.ndarray):
+        import torch
+        t = torch.from_numpy(np.ascontiguousarray(arr))
+        if self.dist.get_backend() == "nccl":
+            t = t.to(self.device if self.device is not None else "cuda")
+        return t
+
+    def allreduce_sum(self, arr: np.ndarray) -> np.ndarray:
+        if self.dist is None or self.world == 1:
+            return arr
+        t = self._tensor(arr)
+        self.dist.all_reduce(t)
+        return t.cpu().numpy()
+
+    def allgather(self, arr: np.ndarray) -> np.ndarray:
+        """Concatenate equal-shaped int arrays from all ranks, in rank order."""
+        if self.dist is None or self.world == 1:
+            return arr
+        t = self._tensor(arr)
+        out = [t.clone() for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return np.concatenate([o.cpu().numpy() for o in out])
+
+
+def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, ebn0_db: float,
+                   batch: int, min_bit_err: int = 200, min_frame_err: int = 40,
+                   max_frames: Optional[int] = None, exact_stop: bool = True, device=None) -> PointResult:
+    """Run one SNR point to the reference's stop rule.
+
+    run_batch(first_cw, n) must decode global frames first_cw..first_cw+n-1 on
+    this rank and return their per-frame results (FRAME_DTYPE). All ranks of
+    an initialised torch.distributed group must call this together."""
+    comm = _Comm(device)
+    acc = np.zeros(6, dtype=np.int64)
+    res = PointResult(ebn0_db, N, T)
+    hist_local = np.zeros(N, dtype=np.int64)   # rounds fully counted: this rank's frames
+    hist_cut = np.zeros(N, dtype=np.int64)     # the cut round: all ranks' frames (gathered)
+    rnd = 0
+    while not stop_reached(acc[0], acc[1], min_bit_err, min_frame_err):
+        if max_frames is not None and acc[3] >= max_frames:
+            break
+        first = rnd * batch * comm.world + comm.rank * batch
+        fr = np.ascontiguousarray(run_batch(first, batch))
+        raw = fr.view(np.int32).reshape(-1, 4)
+        local = np.array([raw[:, 0].sum(), (raw[:, 0] > 0).sum(), raw[:, 1].sum(), len(raw),
+                          T * len(raw), raw[:, 2].sum()], dtype=np.int64)
+        tot = comm.allreduce_sum(local)
+        after = acc + tot
+        crossed = stop_reached(after[0], after[1], min_bit_err, min_frame_err)
+        limit_hit = max_frames is not None and after[3] > max_frames
+        if exact_stop and (crossed or limit_hit):
+            allf = comm.allgather(raw).reshape(-1, 4)
+            if limit_hit:
+                allf = allf[: max(0, max_frames - int(acc[3]))]
+            acc, used = exact_cut(acc, allf, T, min_bit_err, min_frame_err)
+            w = allf[:used, 0]
+            np.add.at(hist_cut, w[w > 0] - 1, 1)
+        else:
+            acc = after
+            w = raw[:, 0]
+            np.add.at(hist_local, w[w > 0] - 1, 1)
+        rnd += 1
+    hist = comm.allreduce_sum(hist_local) + hist_cut
+    res.counts = dict(zip(COUNT_KEYS, (int(x) for x in acc)))
+    res.rounds = rnd
+    res.hist = hist
+    return res
+
+
+def wilson_interval(k: int, n: int, z: float = 1.96):
+    if n == 0:
+        return (float("nan"), float("nan"))
+    p = k / n
+    den = 1 + z * z / n
+    c = (p + z * z / (2 * n)) / den
+    h = z * math.sqrt(p * (1 - p) / n + z * z / (4 * n * n)) / den
+    return (c - h, c + h)
+
+
+def two_proportion_z(k1: int, n1: int, k2: int, n2: int) -> float:
+    """z statistic of H0: p1 == p2 (pooled)."""
+    p = (k1 + k2) / (n1 + n2)
+    se = math.sqrt(p * (1 - p) * (1 / n1 + 1 / n2))
+    return 0.0 if se == 0 else (k1 / n1 - k2 / n2) / se

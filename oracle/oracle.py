@@ -1,0 +1,180 @@
+"""ctypes wrapper of the CPU ORACLE (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package
+(ldpcsimulation_amd/), which must fail loudly without its HIP library instead
+of falling back here. See oracle/ldpc_oracle.h for the reference file:line
+each routine restates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+MS, NMS, OMS = 0, 1, 2
+
+
+class _Rng(C.Structure):
+    _fields_ = [("tbl", C.c_int32 * 31), ("front", C.c_int), ("rear", C.c_int)]
+
+
+class _Alist(C.Structure):
+    _fields_ = [("N", C.c_int), ("M", C.c_int), ("maxdv", C.c_int), ("maxdc", C.c_int),
+                ("deg_n", C.POINTER(C.c_int)), ("deg_m", C.POINTER(C.c_int)),
+                ("nlist", C.POINTER(C.c_int)), ("mlist", C.POINTER(C.c_int))]
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("variant", C.c_int), ("alpha", C.c_double), ("delta", C.c_double),
+                ("quantize", C.c_int), ("saturate", C.c_int), ("ymax", C.c_double),
+                ("qbits", C.c_int)]
+
+
+class _Stats(C.Structure):
+    _fields_ = [("errors", C.c_int64), ("uncoded", C.c_int64), ("bits", C.c_int64),
+                ("words", C.c_int64), ("word_errors", C.c_int64), ("iters", C.c_int64)]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"oracle not built: {path} (run `make -f oracle/Makefile`)")
+        L = C.CDLL(path)
+        L.orc_srandom.argtypes = [C.POINTER(_Rng), C.c_uint32]
+        L.orc_random.argtypes = [C.POINTER(_Rng)]
+        L.orc_random.restype = C.c_int32
+        L.orc_ranf.argtypes = [C.POINTER(_Rng)]
+        L.orc_ranf.restype = C.c_double
+        L.orc_rann.argtypes = [C.POINTER(_Rng)]
+        L.orc_rann.restype = C.c_double
+        L.orc_alist_load.argtypes = [C.c_char_p, C.POINTER(_Alist)]
+        L.orc_alist_free.argtypes = [C.POINTER(_Alist)]
+        L.orc_minsum_run.argtypes = [C.POINTER(_Alist), C.c_double, C.c_double, C.c_int,
+                                     C.POINTER(_Cfg), C.c_uint32, C.c_void_p, C.c_int,
+                                     C.c_int64, C.c_void_p, C.c_int64, C.POINTER(_Stats)]
+        L.orc_minsum_run.restype = C.c_int64
+        L.orc_channel.argtypes = [C.POINTER(_Rng), C.c_int, C.c_double, C.c_void_p, C.c_void_p]
+        L.orc_quantize.argtypes = [C.c_double, C.c_double, C.c_double]
+        L.orc_quantize.restype = C.c_double
+        L.orc_quantize_f32.argtypes = [C.c_float, C.c_float, C.c_float]
+        L.orc_quantize_f32.restype = C.c_float
+        for name in ("orc_decode_f64", "orc_decode_f32"):
+            getattr(L, name).argtypes = [C.POINTER(_Alist), C.c_void_p, C.c_int,
+                                         C.POINTER(_Cfg), C.c_void_p]
+        L.orc_decode_f64_snap.argtypes = [C.POINTER(_Alist), C.c_void_p, C.c_int, C.POINTER(_Cfg),
+                                          C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.orc_philox4x32_10.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        _LIB = L
+    return _LIB
+
+
+class GlibcRandom:
+    """glibc srandom()/random() TYPE_3 restatement + rand.h ranf/rann."""
+
+    def __init__(self, seed: int):
+        self._s = _Rng()
+        lib().orc_srandom(C.byref(self._s), seed & 0xFFFFFFFF)
+
+    def random(self) -> int:
+        return lib().orc_random(C.byref(self._s))
+
+    def ranf(self) -> float:
+        return lib().orc_ranf(C.byref(self._s))
+
+    def rann(self) -> float:
+        return lib().orc_rann(C.byref(self._s))
+
+    def channel(self, c: np.ndarray, sigma: float) -> np.ndarray:
+        c = np.ascontiguousarray(c, dtype=np.int32)
+        y = np.empty(c.shape[0], dtype=np.float64)
+        lib().orc_channel(C.byref(self._s), c.shape[0], sigma, c.ctypes.data, y.ctypes.data)
+        return y
+
+
+@dataclass
+class Cfg:
+    variant: int = MS
+    alpha: float = 1.0
+    delta: float = 0.0
+    quantize: bool = False
+    saturate: bool = False
+    ymax: float = 0.0
+    qbits: int = 0
+
+    def c(self) -> _Cfg:
+        return _Cfg(self.variant, self.alpha, self.delta, int(self.quantize),
+                    int(self.saturate), self.ymax, self.qbits)
+
+
+class Alist:
+    def __init__(self, path: str):
+        self._a = _Alist()
+        if lib().orc_alist_load(path.encode(), C.byref(self._a)) != 0:
+            raise IOError(path)
+        self.N, self.M = self._a.N, self._a.M
+
+    def __del__(self):
+        try:
+            lib().orc_alist_free(C.byref(self._a))
+        except Exception:
+            pass
+
+    def minsum_run(self, R, snr, T, cfg: Cfg, seed, cw_lines=None, max_frames=-1, cap=0):
+        st = _Stats()
+        fw = np.zeros(max(cap, 1), dtype=np.int32)
+        if cw_lines:
+            arr = (C.c_char_p * len(cw_lines))(*[s.encode() for s in cw_lines])
+            cwp, ncw = C.cast(arr, C.c_void_p), len(cw_lines)
+        else:
+            arr, cwp, ncw = None, None, 0
+        n = lib().orc_minsum_run(C.byref(self._a), R, snr, T, C.byref(cfg.c()), seed & 0xFFFFFFFF,
+                                 cwp, ncw, max_frames, fw.ctypes.data if cap else None, cap,
+                                 C.byref(st))
+        return n, {k: getattr(st, k) for k, _ in _Stats._fields_}, fw[:min(n, cap)]
+
+    def decode(self, yq: np.ndarray, T: int, cfg: Cfg) -> np.ndarray:
+        """Decode a [B, N] or [N] batch; dtype float64 or float32 selects precision."""
+        yq = np.ascontiguousarray(yq)
+        single = yq.ndim == 1
+        yq2 = yq.reshape(-1, self.N)
+        d = np.empty(yq2.shape, dtype=np.int8)
+        fn = lib().orc_decode_f64 if yq2.dtype == np.float64 else lib().orc_decode_f32
+        assert yq2.dtype in (np.float64, np.float32)
+        cc = cfg.c()
+        for b in range(yq2.shape[0]):
+            fn(C.byref(self._a), yq2[b].ctypes.data, T, C.byref(cc), d[b].ctypes.data)
+        return d[0] if single else d
+
+    def decode_snap(self, yq: np.ndarray, T: int, cfg: Cfg, snap_it: int):
+        yq = np.ascontiguousarray(yq, dtype=np.float64)
+        E = int(sum(self._a.deg_m[j] for j in range(self.M)))
+        c2v = np.empty(E, dtype=np.float64)
+        app = np.empty(self.N, dtype=np.float64)
+        d = np.empty(self.N, dtype=np.int8)
+        lib().orc_decode_f64_snap(C.byref(self._a), yq.ctypes.data, T, C.byref(cfg.c()),
+                                  d.ctypes.data, snap_it, c2v.ctypes.data, app.ctypes.data)
+        return d, c2v, app
+
+
+def quantize(x: float, ymax: float, qbits: int) -> float:
+    return lib().orc_quantize(x, ymax, 2.0 ** qbits)
+
+
+def quantize_f32(x: float, ymax: float, qbits: int) -> float:
+    return lib().orc_quantize_f32(x, ymax, 2.0 ** qbits)
+
+
+def philox4x32_10(ctr, key) -> list:
+    c = np.ascontiguousarray(np.array(ctr, dtype=np.uint32))
+    k = np.ascontiguousarray(np.array(key, dtype=np.uint32))
+    o = np.empty(4, dtype=np.uint32)
+    lib().orc_philox4x32_10(c.ctypes.data, k.ctypes.data, o.ctypes.data)
+    return [int(x) for x in o]

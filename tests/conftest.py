@@ -1,0 +1,43 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+CODES = os.path.join(GOLD, "codes")
+REFERENCE = "/root/reference/C_implementations"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libldpc_hip.so on the device)")
+
+
+def code_path(name: str) -> str:
+    return os.path.join(CODES, name)
+
+
+def golden_runs():
+    with open(os.path.join(GOLD, "reference_runs.json")) as f:
+        return json.load(f)["runs"]
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx_factory():
+    """Device contexts, cached per (code, max_batch); fails loudly without the HIP library."""
+    from ldpcsimulation_amd import native
+    assert native.device_count() > 0, "no HIP device visible"
+    cache = {}
+
+    def make(code: str, max_batch: int = 4096):
+        key = (code, max_batch)
+        if key not in cache:
+            g = native.Graph.from_alist(code_path(code) if not os.path.isabs(code) else code)
+            cache[key] = native.Context(g, 0, max_batch)
+        return cache[key]
+
+    return make

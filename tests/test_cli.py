@@ -1,0 +1,51 @@
+"""The reference-compatible CLI (bin/decodeMinSum & co.) against the reference's own stdout.
+
+With LDPC_RNG=glibc (default) and LDPC_SEED equal to the reference's seed, the
+GPU front-end must print exactly what the reference printed (golden stdout from
+oracle/_ref, tests/golden/reference_runs.json) and append the same log line.
+"""
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT, code_path, golden_runs
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(ROOT, "bin")
+
+
+@pytest.mark.parametrize("run", [r for r in golden_runs() if not r["binary"].endswith("_g")],
+                         ids=lambda r: r["name"])
+def test_cli_stdout_identical_to_reference(tmp_path, run):
+    alist = code_path(run["code"])
+    log = tmp_path / "log.txt"
+    cmd = [os.path.join(BIN, run["binary"]), alist] + run["args"] + [str(log)]
+    if run["cwfile"]:
+        cmd.append(code_path(run["cwfile"]))
+    env = dict(os.environ, LDPC_SEED=str(run["seed"]), LDPC_RNG="glibc")
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr
+    out = p.stdout.replace(alist, "@ALIST@").replace(str(log), "@LOGFILE@")
+    if run["cwfile"]:
+        out = out.replace(code_path(run["cwfile"]), "@CWFILE@")
+    assert out == run["stdout"]
+    assert log.read_text().replace(alist, "@ALIST@") == run["log_line"]
+
+
+def test_cli_usage_exits_zero():
+    p = subprocess.run([os.path.join(BIN, "decodeMinSum")], capture_output=True, text=True)
+    assert p.returncode == 0
+    assert p.stdout.startswith("Usage: ") and "logfilename [codeword filename]" in p.stdout
+
+
+def test_cli_philox_mode_runs(tmp_path):
+    log = tmp_path / "l.txt"
+    env = dict(os.environ, LDPC_SEED="3", LDPC_RNG="philox", LDPC_BATCH="4096")
+    p = subprocess.run([os.path.join(BIN, "decodeNMS"), code_path("80211n_1944_r12.alist"), "0.5", "1.25", "50",
+                        "1.25", str(log)], env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr
+    assert "Final result:" in p.stdout
+    fields = log.read_text().split("\t")
+    assert fields[0] == "1.25" and fields[4] == "50" and fields[5] == "1.25"

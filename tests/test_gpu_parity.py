@@ -1,0 +1,238 @@
+"""GPU parity: the HIP decoder (through the C ABI) against the oracle and the reference.
+
+Tiers:
+  (a) identical channel samples y -> decisions bit-exact with the oracle, in
+      fp64 (the reference's precision) and fp32 (oracle run in float);
+  (b) whole reference runs (tests/golden/reference_runs.json, produced by the
+      compiled reference) reproduced through the GPU: same totals, same
+      sequence of per-frame error weights;
+  (c) statistical: on-device Philox noise and FER against the reference.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import code_path, golden_runs
+from helpers import cw_lines, final_numbers, run_config
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CODES = ["PEGReg504x1008.alist", "80211n_1944_r12.alist", "4000.2000.4.244.alist"]
+VARIANTS = {
+    "ms": dict(variant=0),
+    "nms": dict(variant=1, alpha=1.25),
+    "oms": dict(variant=2, delta=0.15),
+    "qnms": dict(variant=1, alpha=1.25, quantize=True, ymax=1.5, qbits=4),
+    "qoms": dict(variant=2, delta=0.15, quantize=True, ymax=1.5, qbits=4),
+    "sat_ms": dict(variant=0, saturate=True, ymax=1.2),
+}
+
+
+def _native():
+    from ldpcsimulation_amd import native
+    return native
+
+
+def _glibc_frames(N, nframes, ebn0, R, seed, c=None):
+    g = O.GlibcRandom(seed)
+    sigma = math.sqrt(10 ** (-ebn0 / 10) / R / 2)
+    c = np.ones(N, dtype=np.int32) if c is None else c
+    return np.stack([g.channel(c, sigma) for _ in range(nframes)])
+
+
+def _oracle_front(y, v, f32):
+    if v.get("quantize"):
+        q = O.quantize_f32 if f32 else O.quantize
+        flat = np.array([q(float(x), v["ymax"], v["qbits"]) for x in y.ravel()],
+                        dtype=np.float32 if f32 else np.float64)
+        return flat.reshape(y.shape)
+    if v.get("saturate"):
+        ym = np.float32(v["ymax"]) if f32 else v["ymax"]
+        return np.clip(y, -ym, ym)
+    return y
+
+
+@pytest.mark.parametrize("code", CODES)
+@pytest.mark.parametrize("vname", list(VARIANTS))
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_decisions_bit_exact_vs_oracle(gpu_ctx_factory, code, vname, prec):
+    native = _native()
+    ctx = gpu_ctx_factory(code)
+    N = ctx.graph.N
+    v = VARIANTS[vname]
+    f32 = prec == "f32"
+    y = _glibc_frames(N, 12, 1.8, 0.5, seed=1234 + len(vname))
+    if f32:
+        y = y.astype(np.float32)
+    A = O.Alist(code_path(code))
+    yq = _oracle_front(y, v, f32)
+    for T in (0, 1, 3, 10):
+        cfg = native.DecoderConfig(T=T, precision=native.F32 if f32 else native.F64, **v)
+        d, fr, cnt = ctx.decode(y, cfg)
+        want = A.decode(yq, T, O.Cfg(**{k: v[k] for k in v}))
+        mism = int((d != want).sum())
+        assert mism == 0, f"T={T}: {mism} decision mismatches"
+        w = (want != 1).sum(axis=1)
+        assert np.array_equal(fr["bit_err"], w)
+        assert cnt.frames == len(y) and cnt.bit_err == int(w.sum())
+        assert cnt.frame_err == int((w > 0).sum()) and cnt.iters == T * len(y)
+
+
+@pytest.mark.parametrize("run", golden_runs(), ids=lambda r: r["name"])
+def test_gpu_reproduces_reference_run(gpu_ctx_factory, run):
+    """The reference's own Monte-Carlo run, with the reference's noise, decoded on the GPU in fp64."""
+    native = _native()
+    R, snr, T, c = run_config(run)
+    bit_ref, words_ref, unc_ref = final_numbers(run["final"])
+    ctx = gpu_ctx_factory(run["code"], 1024)
+    N = ctx.graph.N
+    lines = cw_lines(run)
+    g = O.GlibcRandom(run["seed"])
+    sigma = math.sqrt(10 ** (-snr / 10) / R / 2)
+    cfg = native.DecoderConfig(T=T, precision=native.F64, **c)
+    errors = words = word_errors = unc = 0
+    ferr = []
+    f = 0
+    done = False
+    while not done:
+        B = 256
+        cw = np.ones((B, N), dtype=np.int8)
+        ys = np.empty((B, N))
+        for k in range(B):
+            if lines:
+                cw[k] = [-1 if ch == "1" else 1 for ch in lines[(f + k) % len(lines)][:N]]
+            ys[k] = g.channel(cw[k].astype(np.int32), sigma)
+        _, fr, _ = ctx.decode(ys, cfg, c=cw if lines else None, want_decisions=False)
+        f += B
+        for r in fr:
+            if not (errors < 200 or word_errors < 40):
+                done = True
+                break
+            unc += int(r["uncoded_bit_err"])
+            if r["bit_err"] > 0:
+                errors += int(r["bit_err"])
+                word_errors += 1
+                ferr.append(int(r["bit_err"]))
+            words += 1
+    assert (errors, words, unc) == (bit_ref, words_ref, unc_ref)
+    assert ferr == run["ferr_weights"]
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_fused_sim_matches_oracle_on_device_noise(gpu_ctx_factory, prec):
+    """AWGN -> decode -> count in one kernel: decisions equal the oracle's on the y it generated."""
+    native = _native()
+    ctx = gpu_ctx_factory("80211n_1944_r12.alist")
+    f32 = prec == "f32"
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=20,
+                               precision=native.F32 if f32 else native.F64)
+    y, d, fr, cnt = ctx.sim_trace(1.25, 0.5, cfg, seed=77, stream_id=3, first_cw=1000, batch=24)
+    A = O.Alist(code_path("80211n_1944_r12.alist"))
+    want = A.decode(y, 20, O.Cfg(variant=1, alpha=1.25))
+    assert int((d != want).sum()) == 0
+    w = (want != 1).sum(axis=1)
+    assert np.array_equal(fr["bit_err"], w)
+    assert np.array_equal(fr["uncoded_bit_err"], (y <= 0).sum(axis=1))
+    assert cnt.bit_err == int(w.sum()) and cnt.frames == 24
+
+
+def test_sim_independent_of_batch_split(gpu_ctx_factory):
+    native = _native()
+    ctx = gpu_ctx_factory("80211n_1944_r12.alist")
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=10)
+    full, c_full = ctx.sim_batch(1.0, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=512)
+    a, c_a = ctx.sim_batch(1.0, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=200)
+    b, c_b = ctx.sim_batch(1.0, 0.5, cfg, seed=5, stream_id=0, first_cw=200, batch=312)
+    assert np.array_equal(full, np.concatenate([a, b]))
+    assert c_full.bit_err == c_a.bit_err + c_b.bit_err
+    other, _ = ctx.sim_batch(1.0, 0.5, cfg, seed=6, stream_id=0, first_cw=0, batch=512)
+    assert not np.array_equal(full["uncoded_bit_err"], other["uncoded_bit_err"])
+
+
+@pytest.mark.parametrize("code", CODES)
+def test_all_kernels_bit_identical(monkeypatch, code):
+    """The row-parallel, per-codeword-LDS and global-memory kernels give identical results."""
+    native = _native()
+    g = native.Graph.from_alist(code_path(code))
+    ctxs = {}
+    for k in ("default", "lds", "global"):
+        if k == "default":
+            monkeypatch.delenv("LDPC_KERNEL", raising=False)
+        else:
+            monkeypatch.setenv("LDPC_KERNEL", k)
+        ctxs[k] = native.Context(g, 0, 300)
+    monkeypatch.delenv("LDPC_KERNEL", raising=False)
+    cfg = native.DecoderConfig(variant=native.OMS, delta=0.1, T=15, quantize=True, ymax=1.5, qbits=5)
+    for prec in (native.F32, native.F64):
+        cfg.precision = prec
+        names = {k: c.kernel_info(cfg)["kernel"] for k, c in ctxs.items()}
+        assert names["lds"] == "lds" and names["global"] == "global"
+        if code != "4000.2000.4.244.alist":
+            assert names["default"] == "rows"
+        outs = {k: c.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300) for k, c in ctxs.items()}
+        ref = outs["global"]
+        for k, o in outs.items():
+            for a, b in zip(o[:3], ref[:3]):
+                assert np.array_equal(a, b), k
+
+
+def test_channel_noise_statistics(gpu_ctx_factory):
+    """Philox + Box-Muller noise: mean/variance/tails of (y-1)/sigma over 24M samples."""
+    native = _native()
+    ctx = gpu_ctx_factory("80211n_1944_r12.alist", 4096)
+    cfg = native.DecoderConfig(T=0, precision=native.F64)
+    sigma = math.sqrt(10 ** (-1.5 / 10) / 0.5 / 2)
+    n = []
+    for k in range(3):
+        y, _, _, _ = ctx.sim_trace(1.5, 0.5, cfg, seed=11, stream_id=k, first_cw=0, batch=4096)
+        n.append(((y - 1.0) / sigma).ravel())
+    n = np.concatenate(n)
+    m = n.size
+    assert abs(n.mean()) < 5 / math.sqrt(m)
+    assert abs(n.var() - 1) < 5 * math.sqrt(2 / m)
+    for t in (1.0, 2.0, 3.0):
+        p = math.erfc(t / math.sqrt(2))
+        got = float((np.abs(n) > t).mean())
+        assert abs(got - p) < 6 * math.sqrt(p * (1 - p) / m), (t, got, p)
+    # independence of consecutive samples
+    assert abs(np.corrcoef(n[:-1], n[1:])[0, 1]) < 5 / math.sqrt(m)
+
+
+def test_syndrome_and_codeword_mode(gpu_ctx_factory):
+    """Codeword-file mode decodes the transmitted codeword; decoded frames have zero syndrome."""
+    native = _native()
+    ctx = gpu_ctx_factory("PEGReg504x1008.alist", 2048)
+    lines = [l.strip() for l in open(code_path("PEGReg504x1008_data20.enc")) if l.strip()]
+    bits = np.array([[int(ch) for ch in l] for l in lines], dtype=np.uint8)
+    ctx.set_codewords(bits)
+    try:
+        cfg = native.DecoderConfig(T=20)
+        y, d, fr, cnt = ctx.sim_trace(2.5, 0.5, cfg, seed=3, stream_id=0, first_cw=0, batch=400)
+        rows = np.arange(400) % len(lines)
+        c = 1 - 2 * bits[rows].astype(np.int8)
+        assert np.array_equal(fr["bit_err"], (d != c).sum(axis=1))
+        ok = fr["bit_err"] == 0
+        assert ok.sum() > 300
+        assert (fr["syndrome_fail"][ok] == 0).all()
+        # channel symmetry: the same noise on the all-zero word gives the same weights
+        ctx.set_codewords(None)
+        fr0, _ = ctx.sim_batch(2.5, 0.5, cfg, 3, 0, 0, 400)
+        assert np.array_equal(fr0["bit_err"], fr["bit_err"])
+    finally:
+        ctx.set_codewords(None)
+
+
+def test_fer_matches_reference_statistically(gpu_ctx_factory):
+    """802.11n N=1944 NMS a=1.25 T=50: GPU fp32 Philox FER vs the reference's (REF_SEED=11):
+    two-proportion z-test |z| < 3 at 1.0/1.25/1.5 dB."""
+    native = _native()
+    from ldpcsimulation_amd.sim import two_proportion_z
+    ctx = gpu_ctx_factory("80211n_1944_r12.alist", 16384)
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50)
+    ref = {1.0: (40, 96), 1.25: (40, 362), 1.5: (40, 2212)}
+    for ebn0, (k_ref, n_ref) in ref.items():
+        _, cnt = ctx.sim_batch(ebn0, 0.5, cfg, seed=2026, stream_id=int(ebn0 * 100), first_cw=0, batch=16384)
+        z = two_proportion_z(cnt.frame_err, cnt.frames, k_ref, n_ref)
+        assert abs(z) < 3, (ebn0, cnt.frame_err, cnt.frames, z)
