@@ -79,6 +79,8 @@ struct ldpc_ctx {
     bool has_rs = false;
     ldpc::RowSched rs{};
     DevBuf sched;
+    DevBuf divcheck;                                      // mismatch counter of verify_div_by_reciprocal
+    std::vector<std::pair<float, bool>> div_ok;           // alpha -> reciprocal division exact
 };
 
 extern "C" {
@@ -165,7 +167,7 @@ static void ctx_free(ldpc_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->graph, &c->counts, &c->hist, &c->y_stage, &c->c_stage, &c->d_stage, &c->fw_stage,
-                      &c->cw_table, &c->gscratch, &c->sched})
+                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -340,6 +342,35 @@ static void fill_common(ldpc::DecodeArgs &a, ldpc_ctx *c, const ldpc_decoder_cfg
 
 static_assert(sizeof(ldpc_frame_result) == sizeof(int4), "frame result layout");
 
+// fp32 NMS: use the reciprocal division only after the device has checked it
+// against IEEE x/alpha for every finite non-negative float (cached per alpha).
+static int nms_setup(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, ldpc::DecodeArgs &a)
+{
+    a.nms_fast = 0;
+    a.alpha_rcp = 0.f;
+    if (cfg->variant != LDPC_NMS || cfg->precision != LDPC_F32) return LDPC_OK;
+    const float alpha = (float)cfg->alpha;
+    if (!(alpha > 0.f) || !std::isfinite(alpha)) return LDPC_OK;
+    const float rcp = 1.0f / alpha;
+    bool ok = false, known = false;
+    for (const auto &e : c->div_ok)
+        if (e.first == alpha) { ok = e.second; known = true; }
+    if (!known) {
+        HIP_TRY(c->divcheck.ensure(sizeof(unsigned long long)));
+        HIP_TRY(ldpc::verify_div_by_reciprocal(alpha, rcp, (unsigned long long *)c->divcheck.p, c->stream));
+        unsigned long long bad = 1;
+        HIP_TRY(hipMemcpyAsync(&bad, c->divcheck.p, sizeof bad, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        ok = bad == 0;
+        c->div_ok.emplace_back(alpha, ok);
+    }
+    if (ok) {
+        a.nms_fast = 1;
+        a.alpha_rcp = rcp;
+    }
+    return LDPC_OK;
+}
+
 static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64)
 {
     const ldpc::KernelChoice kc =
@@ -405,6 +436,10 @@ int ldpc_decode_batch(ldpc_ctx *c, const void *y, int batch, const ldpc_decoder_
     ldpc::DecodeArgs a;
     fill_common(a, c, cfg, batch);
     a.src = ldpc::SRC_GIVEN;
+    {
+        const int nrc = nms_setup(c, cfg, a);
+        if (nrc) return nrc;
+    }
     // Inputs: stage host buffers.
     if (is_device_ptr(y)) {
         a.y = y;
@@ -495,6 +530,10 @@ static int sim_launch_impl(ldpc_ctx *c, double ebn0_db, double R, const ldpc_dec
     ldpc::DecodeArgs a;
     fill_common(a, c, cfg, batch);
     a.src = ldpc::SRC_PHILOX;
+    {
+        const int nrc = nms_setup(c, cfg, a);
+        if (nrc) return nrc;
+    }
     const double N0 = std::pow(10.0, -ebn0_db / 10.0) / R;   // :146
     a.sigma = std::sqrt(N0 / 2.0);                            // :147
     a.seed = seed;

@@ -93,7 +93,7 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
     if (threads % 64 || threads < g.M) return "rows exceed threads";
     if ((long)threads * cpt < g.N) return "bits exceed slots";
     if (g.maxdc > dc) return "row degree exceeds kernel bound";
-    if (g.N > 65535) return "N exceeds 16-bit schedule";
+    if (g.N > 65534) return "N exceeds 16-bit schedule";
     s = RowSchedule();
     s.threads = threads;
     s.cpt = cpt;
@@ -115,13 +115,22 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
         gbase[grp + 1] = gbase[grp] + 64 * md;
     }
     s.e_pad = gbase[ngroups];
-    if (s.e_pad > 65535) return "padded edge count exceeds 16-bit schedule";
+    if (s.e_pad + 64 > 65535) return "padded edge count exceeds 16-bit schedule";
     if (s.e_pad < g.N) s.e_pad = g.N;   // the c2v area doubles as channel staging
     s.vn_col.assign(nslots, 0xffff);
     s.vn_info.assign(nslots, 0);
+    for (int slot = g.N; slot < nslots; ++slot)   // empty slots: degree 0, reads stay inside their group
+        s.vn_info[(size_t)(slot % threads) * cpt + slot / threads] =
+            (uint32_t)(gbase[slot >> 6] + (slot & 63)) |
+            ((uint32_t)((gbase[(slot >> 6) + 1] - gbase[slot >> 6]) / 64) << 24);
     s.cn_cols.assign((size_t)threads * dc, 0);
     s.cn_pos.assign((size_t)threads * dc, 0);
     s.cn_deg.assign(threads, 0);
+    for (int t = 0; t < threads; ++t)   // padding edges: read the +INF sentinel bit N, write the lane's dummy slot
+        for (int k = 0; k < dc; ++k) {
+            s.cn_cols[(size_t)t * dc + k] = (uint16_t)g.N;
+            s.cn_pos[(size_t)t * dc + k] = (uint16_t)(s.e_pad + (t & 63));
+        }
     for (int j = 0; j < g.M; ++j) {
         s.cn_deg[j] = g.row_deg[j];
         for (int k = 0; k < g.row_deg[j]; ++k)
@@ -134,7 +143,8 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
         const int t = slot % threads, i = slot / threads;
         const int idx = t * cpt + i;   // stored thread-major so a thread's slots are contiguous
         s.vn_col[idx] = (uint16_t)v;
-        s.vn_info[idx] = (uint32_t)gbase[grp] | ((uint32_t)g.col_deg[v] << 16);
+        const uint32_t gdeg = (uint32_t)((gbase[grp + 1] - gbase[grp]) / 64);
+        s.vn_info[idx] = (uint32_t)(gbase[grp] + lane) | ((uint32_t)g.col_deg[v] << 16) | (gdeg << 24);
         for (int kc = 0; kc < g.col_deg[v]; ++kc) {
             const uint32_t ref = g.col_refs[g.col_ptr[v] + kc];
             const int j = (int)(ref >> kRefShift), kr = (int)(ref & ((1u << kRefShift) - 1));

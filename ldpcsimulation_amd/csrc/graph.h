@@ -41,7 +41,7 @@ struct RowSchedule {
     std::vector<uint16_t> cn_pos;    // [threads * dc]  c2v element of row edge k
     std::vector<uint8_t> cn_deg;     // [threads]
     std::vector<uint16_t> vn_col;    // [threads * cpt] column of slot s (0xffff = none)
-    std::vector<uint32_t> vn_info;   // [threads * cpt] gbase | deg << 16
+    std::vector<uint32_t> vn_info;   // [threads * cpt] (gbase+lane) | deg << 16 | group degree << 24
 };
 
 // Build from alist_struct-style arrays (1-based). Returns "" on success or

@@ -18,6 +18,10 @@ enum { SRC_GIVEN = 0, SRC_PHILOX = 1 };
 struct DecodeArgs {
     int batch, T, variant, quantize, saturate;
     double ymax, nq, alpha, delta;
+    // fp32 NMS: q = x*r, q += fma(-q, alpha, x)*r equals x/alpha for every
+    // finite float x (verified on the device by verify_div_by_reciprocal)
+    int nms_fast;
+    float alpha_rcp;
     int src;
     const void *y;                  // SRC_GIVEN: [batch][N] float|double (device)
     const int8_t *c;                // SRC_GIVEN: [batch][N] bipolar, or null (+1)
@@ -60,6 +64,12 @@ hipError_t launch_decode(const DevGraph &g, const DecodeArgs &a, bool f64, const
                          void *gscratch, int gscratch_blocks, hipStream_t s, const RowSched *rs = nullptr,
                          int num_cus = 256);
 int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc);
+
+// Exhaustive device check that dividing by alpha through its correctly rounded
+// reciprocal plus one FMA correction step reproduces IEEE x/alpha for all
+// 2^31 - 2^23 finite non-negative floats x (the only operands the check-node
+// normalisation divides: |v2c| minima). *mismatches receives the count.
+hipError_t verify_div_by_reciprocal(float alpha, float rcp, unsigned long long *mismatches_dev, hipStream_t s);
 
 // Row-kernel template bounds (host picks the smallest that fits).
 constexpr int kRowsMaxThreads = 1024;

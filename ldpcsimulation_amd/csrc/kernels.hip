@@ -322,21 +322,45 @@ __device__ __forceinline__ int u16_at(const uint32_t (&w)[DC / 2], int k)
     return (int)((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
 }
 
+// The C codewords of a block are interleaved in LDS: one Pack = the same
+// element of all C codewords, so every gather/scatter moves C values
+// (ds_read_b64 / ds_write_b64 for two fp32 codewords or one fp64).
+template <typename F, int C> struct __attribute__((aligned(sizeof(F) * C))) Pack { F v[C]; };
+
+// x / alpha for the check-node normalisation (:498). fp32 with a verified
+// alpha: reciprocal + one FMA correction (3 VALU instead of ~10); otherwise,
+// and for non-finite minima, the IEEE division.
+template <typename F>
+__device__ __forceinline__ F nms_div(F x, F alpha, const DecodeArgs &a)
+{
+    return x / alpha;
+}
+template <>
+__device__ __forceinline__ float nms_div<float>(float x, float alpha, const DecodeArgs &a)
+{
+    if (a.nms_fast && x < __builtin_huge_valf()) {
+        const float q = x * a.alpha_rcp;
+        return __builtin_fmaf(__builtin_fmaf(-q, alpha, x), a.alpha_rcp, q);
+    }
+    return x / alpha;
+}
+
 template <typename F, int SRC, int C, int DC, int CPT>
 __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, RowSched rs)
 {
     using MT = typename MetaOf<DC>::T;
-    constexpr int SH = MetaOf<DC>::SH;
-    constexpr MT NONE = (MT)((1u << SH) - 1u);
+    using P = Pack<F, C>;
+    constexpr MT NONE = (MT)((1u << MetaOf<DC>::SH) - 1u);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
-    const int N = g.N, EP = rs.e_pad;
-    F *app = reinterpret_cast<F *>(smem);        // [C][N]
-    F *c2v = app + C * N;                         // [C][EP]
-    int *red = reinterpret_cast<int *>(c2v + C * EP);
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int N = g.N, EA = rs.e_pad + 64;         // + one dummy slot per lane for padding edges
+    P *app = reinterpret_cast<P *>(smem);          // [N + 1]: bit N is the +INF sentinel of padding edges
+    P *c2v = app + (N + 2);                        // [EA] (N+2 keeps 16-B alignment)
+    int *red = reinterpret_cast<int *>(c2v + EA);
 
     // ---- the thread's share of the graph, in registers for the whole launch ----
     const int deg = rs.cn_deg[tid];
+    const MT degmask = (deg >= (int)(8 * sizeof(MT))) ? ~(MT)0 : (((MT)1 << deg) - 1);
     uint32_t colw[DC / 2], posw[DC / 2];
 #pragma unroll
     for (int q = 0; q < DC / 8; ++q) {
@@ -353,6 +377,12 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
         vcol[i] = c == 0xffff ? -1 : c;
         vinfo[i] = rs.vn_info[tid * CPT + i];
     }
+    if (tid == 0) {
+        P inf;
+#pragma unroll
+        for (int c = 0; c < C; ++c) inf.v[c] = dinf<F>();
+        app[N] = inf;
+    }
 
     const F alpha = (F)a.alpha, delta = (F)a.delta;
     const int ngrp = (a.batch + C - 1) / C;
@@ -367,13 +397,12 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
             const int b = grp * C + c;
             if (b >= a.batch) continue;
             const uint64_t cw = a.first_cw + (uint64_t)b;
-            F *stage = c2v + c * EP;
             if (SRC == SRC_GIVEN) {
                 if (a.c) cvec[c] = a.c + (size_t)b * N;
                 const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
                 for (int v = tid; v < N; v += nt) {
                     const F q = front_end<F>(y[v], a);
-                    stage[v] = q;
+                    c2v[v].v[c] = q;
                     const int cv = cvec[c] ? cvec[c][v] : 1;
                     unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
                 }
@@ -395,7 +424,7 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
                             const F yv = (F)cv * (F(1) + sigma * n[q4]);
                             if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
                             const F q = front_end<F>(yv, a);
-                            stage[v] = q;
+                            c2v[v].v[c] = q;
                             unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
                         }
                     }
@@ -405,48 +434,59 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
         __syncthreads();
         F yq[C][CPT];
 #pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int v = vcol[i];
+            const P st = c2v[v >= 0 ? v : 0];
+#pragma unroll
+            for (int c = 0; c < C; ++c) yq[c][i] = st.v[c];
+            if (v >= 0) app[v] = st;   // v2c = yq on the first pass (:364-370)
+        }
+        __syncthreads();
+        // Padding slots of the bit-node layout hold +0 (adding +0 leaves every
+        // sum, and hence every decision, unchanged).
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int base = (int)(vinfo[i] & 0xffffu), dg = (int)((vinfo[i] >> 16) & 0xffu);
+            const int gd = (int)(vinfo[i] >> 24);
+            P z;
+#pragma unroll
+            for (int c = 0; c < C; ++c) z.v[c] = F(0);
+            for (int k = dg; k < gd; ++k) c2v[base + k * 64] = z;
+        }
+
+        // c2v sent on each edge last iteration (the check node's own copy): +0 before the first.
+        F prev[C][DC];
+#pragma unroll
         for (int c = 0; c < C; ++c)
 #pragma unroll
-            for (int i = 0; i < CPT; ++i) {
-                const int v = vcol[i];
-                yq[c][i] = v >= 0 ? c2v[c * EP + v] : F(0);
-                if (v >= 0) app[c * N + v] = yq[c][i];   // v2c = yq on the first pass (:364-370)
-            }
-        __syncthreads();
-
-        F m1[C], m2[C];
-        MT meta[C];
-#pragma unroll
-        for (int c = 0; c < C; ++c) { m1[c] = F(0); m2[c] = F(0); meta[c] = 0; }   // c2v_old = +0
+            for (int k = 0; k < DC; ++k) prev[c][k] = F(0);
 
         for (int it = 0; it < a.T; ++it) {
             // ---- check nodes (:410-450, :494-515) ----
+            P xin[DC];
+#pragma unroll
+            for (int k = 0; k < DC; ++k) xin[k] = app[u16_at<DC>(colw, k)];   // padding edges read +INF
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const F *appc = app + c * N;
-                const int oidx = (int)(meta[c] & NONE);
                 F mn1 = dinf<F>(), mn2 = dinf<F>();
                 MT amin = NONE, sg = 0;
 #pragma unroll
                 for (int k = 0; k < DC; ++k) {
-                    if (k < deg) {
-                        const F mo = (k == oidx) ? m2[c] : m1[c];
-                        const F cold = ((meta[c] >> (SH + k)) & 1u) ? -mo : mo;
-                        const F x = appc[u16_at<DC>(colw, k)] - cold;        // v2c (:469)
-                        sg |= (MT)(!(x >= F(0))) << k;                        // sgn(v2c) (:518-523)
-                        const F ax = dabs(x);
-                        const bool le = ax <= mn1;                            // :428
-                        mn2 = le ? mn1 : ((ax < mn2) ? ax : mn2);             // :430, :434-437
-                        mn1 = le ? ax : mn1;
-                        amin = le ? (MT)k : amin;
-                    }
+                    const F x = xin[k].v[c] - prev[c][k];                      // v2c (:469)
+                    sg |= (MT)(!(x >= F(0))) << k;                              // sgn(v2c) (:518-523)
+                    const F ax = dabs(x);
+                    const bool le = ax <= mn1;                                  // :428-433
+                    const F m2c = (ax < mn2) ? ax : mn2;                        // :434-437
+                    mn2 = le ? mn1 : m2c;
+                    mn1 = le ? ax : mn1;
+                    amin = le ? (MT)k : amin;
                 }
-                const MT degmask = (deg >= (int)(8 * sizeof(MT))) ? ~(MT)0 : (((MT)1 << deg) - 1);
-                MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask) : sg;
+                sg &= degmask;
+                MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask) : sg;   // prod*sgn(v2c_k)
                 F M1 = mn1, M2 = mn2;
                 if (a.variant == V_NMS) {
-                    M1 = mn1 / alpha;
-                    M2 = mn2 / alpha;
+                    M1 = nms_div<F>(mn1, alpha, a);
+                    M2 = nms_div<F>(mn2, alpha, a);
                 } else if (a.variant == V_OMS) {
                     const F t1 = mn1 - delta, t2 = mn2 - delta;
                     const bool p1 = t1 > F(0), p2 = t2 > F(0);
@@ -456,32 +496,45 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
                     if (!p1 || mn1 == F(0)) eff &= abit;
                     if (!p2 || mn2 == F(0)) eff &= ~abit;
                 }
-                F *c2vc = c2v + c * EP;
 #pragma unroll
                 for (int k = 0; k < DC; ++k) {
-                    if (k < deg) {
-                        const F mag = ((MT)k == amin) ? M2 : M1;
-                        c2vc[u16_at<DC>(posw, k)] = ((eff >> k) & 1u) ? -mag : mag;
-                    }
+                    const F mag = ((MT)k == amin) ? M2 : M1;
+                    prev[c][k] = ((eff >> k) & 1u) ? -mag : mag;
                 }
-                m1[c] = M1;
-                m2[c] = M2;
-                meta[c] = amin | (eff << SH);
+            }
+#pragma unroll
+            for (int k = 0; k < DC; ++k) {            // padding edges write the lane's dummy slot
+                P o;
+#pragma unroll
+                for (int c = 0; c < C; ++c) o.v[c] = prev[c][k];
+                c2v[u16_at<DC>(posw, k)] = o;
             }
             __syncthreads();
             // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
 #pragma unroll
             for (int i = 0; i < CPT; ++i) {
                 const int v = vcol[i];
-                if (v >= 0) {
-                    const int gb = (int)(vinfo[i] & 0xffffu) + lane, dg = (int)(vinfo[i] >> 16);
+                const int base = (int)(vinfo[i] & 0xffffu);
+                const int gd = __builtin_amdgcn_readfirstlane((int)(vinfo[i] >> 24));   // wave-uniform
+                F sum[C];
 #pragma unroll
-                    for (int c = 0; c < C; ++c) {
-                        const F *cc = c2v + c * EP + gb;
-                        F sum = yq[c][i];
-                        for (int k = 0; k < dg; ++k) sum += cc[k * 64];
-                        app[c * N + v] = sum;
-                    }
+                for (int c = 0; c < C; ++c) sum[c] = yq[c][i];
+                for (int k0 = 0; k0 < gd; k0 += 4) {   // 4 reads in flight; edges beyond a bit's degree hold +0
+                    P r[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) r[j] = c2v[base + (k0 + j < gd ? k0 + j : k0) * 64];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if (k0 + j < gd) {
+#pragma unroll
+                            for (int c = 0; c < C; ++c) sum[c] += r[j].v[c];
+                        }
+                }
+                if (v >= 0) {
+                    P o;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) o.v[c] = sum[c];
+                    app[v] = o;
                 }
             }
             __syncthreads();
@@ -498,7 +551,7 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
                 for (int i = 0; i < CPT; ++i) {
                     const int v = vcol[i];
                     if (v >= 0) {
-                        const int d = app[c * N + v] > F(0) ? 1 : -1;
+                        const int d = app[v].v[c] > F(0) ? 1 : -1;
                         const int cv = cvec[c] ? cvec[c][v] : 1;
                         w += (d != cv);
                         if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
@@ -507,7 +560,7 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
                 int par = 0;
 #pragma unroll
                 for (int k = 0; k < DC; ++k)
-                    if (k < deg) par ^= (app[c * N + u16_at<DC>(colw, k)] > F(0)) ? 0 : 1;
+                    if (k < deg) par ^= (app[u16_at<DC>(colw, k)].v[c] > F(0)) ? 0 : 1;
                 synd = par;
             }
             w = block_sum(w, red);
@@ -528,6 +581,30 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
     }
 }
 
+// Exhaustive check of the reciprocal division (see kernels.h).
+__global__ __launch_bounds__(256) void k_verify_div(float alpha, float rcp, unsigned long long *bad)
+{
+    const uint32_t total = 0x7f800000u;   // all finite non-negative floats
+    unsigned long long nbad = 0;
+    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += gridDim.x * blockDim.x) {
+        const float x = __uint_as_float(u);
+        const float q = x * rcp;
+        const float f = __builtin_fmaf(__builtin_fmaf(-q, alpha, x), rcp, q);
+        const float d = x / alpha;
+        nbad += (__float_as_uint(f) != __float_as_uint(d));
+    }
+    for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o, 64);
+    if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
+}
+
+hipError_t verify_div_by_reciprocal(float alpha, float rcp, unsigned long long *bad, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(bad, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_verify_div, dim3(8192), dim3(256), 0, s, alpha, rcp, bad);
+    return hipGetLastError();
+}
+
 static size_t state_bytes(const DevGraph &g, bool f64)
 {
     const size_t rs = f64 ? sizeof(RowState<double>) : sizeof(RowState<float>);
@@ -545,7 +622,7 @@ static int rows_cw_per_block(bool f64, int dc) { return (!f64 && dc == 8) ? 2 : 
 static size_t rows_lds(const DevGraph &g, const RowSched &rs, bool f64, int C)
 {
     const size_t fs = f64 ? 8 : 4;
-    return ((size_t)C * ((size_t)g.N + (size_t)rs.e_pad) * fs + 64 + 15) & ~(size_t)15;
+    return ((size_t)C * ((size_t)g.N + 2 + (size_t)rs.e_pad + 64) * fs + 64 + 15) & ~(size_t)15;
 }
 
 KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force)
