@@ -104,25 +104,35 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
     std::stable_sort(order.begin(), order.end(),
                      [&](int a, int b) { return g.col_deg[a] > g.col_deg[b]; });
     const int nslots = threads * cpt;
-    const int ngroups = nslots / 64;
-    std::vector<int> gbase(ngroups + 1, 0);
+    const int waves = threads / 64;
+    const int ngroups = (g.N + 63) / 64;
+    if (ngroups > waves * cpt) return "bits exceed slots";
+    // Degree of each 64-column group (columns in decreasing-degree order) and
+    // the base of its c2v block: edge kc of the group's lane l is at gbase + kc*64 + l.
+    std::vector<int> gdeg(ngroups, 0), gbase(ngroups + 1, 0);
     for (int grp = 0; grp < ngroups; ++grp) {
-        int md = 0;
         for (int l = 0; l < 64; ++l) {
             const int slot = grp * 64 + l;
-            if (slot < g.N) md = std::max(md, (int)g.col_deg[order[slot]]);
+            if (slot < g.N) gdeg[grp] = std::max(gdeg[grp], (int)g.col_deg[order[slot]]);
         }
-        gbase[grp + 1] = gbase[grp] + 64 * md;
+        gbase[grp + 1] = gbase[grp] + 64 * gdeg[grp];
     }
     s.e_pad = gbase[ngroups];
     if (s.e_pad + 64 > 65535) return "padded edge count exceeds 16-bit schedule";
     if (s.e_pad < g.N) s.e_pad = g.N;   // the c2v area doubles as channel staging
+    // Longest-processing-time assignment of groups to waves (a wave's bit-node
+    // phase costs the sum of its groups' degrees), at most cpt groups per wave.
+    std::vector<int> load(waves, 0), used(waves, 0), gw(ngroups), gi(ngroups);
+    for (int grp = 0; grp < ngroups; ++grp) {   // groups are already in decreasing degree
+        int best = -1;
+        for (int w = 0; w < waves; ++w)
+            if (used[w] < cpt && (best < 0 || load[w] < load[best])) best = w;
+        gw[grp] = best;
+        gi[grp] = used[best]++;
+        load[best] += gdeg[grp];
+    }
     s.vn_col.assign(nslots, 0xffff);
-    s.vn_info.assign(nslots, 0);
-    for (int slot = g.N; slot < nslots; ++slot)   // empty slots: degree 0, reads stay inside their group
-        s.vn_info[(size_t)(slot % threads) * cpt + slot / threads] =
-            (uint32_t)(gbase[slot >> 6] + (slot & 63)) |
-            ((uint32_t)((gbase[(slot >> 6) + 1] - gbase[slot >> 6]) / 64) << 24);
+    s.vn_info.assign(nslots, 0);   // unused positions: group degree 0 (skipped)
     s.cn_cols.assign((size_t)threads * dc, 0);
     s.cn_pos.assign((size_t)threads * dc, 0);
     s.cn_deg.assign(threads, 0);
@@ -136,19 +146,20 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
         for (int k = 0; k < g.row_deg[j]; ++k)
             s.cn_cols[(size_t)j * dc + k] = (uint16_t)g.row_cols[(size_t)j * std::max(g.maxdc, 1) + k];
     }
-    // slot s = t + threads*i  <->  thread t, slot index i
-    for (int slot = 0; slot < g.N; ++slot) {
-        const int v = order[slot];
-        const int grp = slot >> 6, lane = slot & 63;
-        const int t = slot % threads, i = slot / threads;
-        const int idx = t * cpt + i;   // stored thread-major so a thread's slots are contiguous
-        s.vn_col[idx] = (uint16_t)v;
-        const uint32_t gdeg = (uint32_t)((gbase[grp + 1] - gbase[grp]) / 64);
-        s.vn_info[idx] = (uint32_t)(gbase[grp] + lane) | ((uint32_t)g.col_deg[v] << 16) | (gdeg << 24);
-        for (int kc = 0; kc < g.col_deg[v]; ++kc) {
-            const uint32_t ref = g.col_refs[g.col_ptr[v] + kc];
-            const int j = (int)(ref >> kRefShift), kr = (int)(ref & ((1u << kRefShift) - 1));
-            s.cn_pos[(size_t)j * dc + kr] = (uint16_t)(gbase[grp] + kc * 64 + lane);
+    for (int grp = 0; grp < ngroups; ++grp) {
+        for (int l = 0; l < 64; ++l) {
+            const int slot = grp * 64 + l;
+            const int t = gw[grp] * 64 + l;
+            const size_t idx = (size_t)t * cpt + gi[grp];   // thread-major: a thread's slots are contiguous
+            const int v = slot < g.N ? order[slot] : -1;
+            const int d = v >= 0 ? g.col_deg[v] : 0;
+            s.vn_col[idx] = v >= 0 ? (uint16_t)v : (uint16_t)0xffff;
+            s.vn_info[idx] = (uint32_t)(gbase[grp] + l) | ((uint32_t)d << 16) | ((uint32_t)gdeg[grp] << 24);
+            for (int kc = 0; kc < d; ++kc) {
+                const uint32_t ref = g.col_refs[g.col_ptr[v] + kc];
+                const int j = (int)(ref >> kRefShift), kr = (int)(ref & ((1u << kRefShift) - 1));
+                s.cn_pos[(size_t)j * dc + kr] = (uint16_t)(gbase[grp] + kc * 64 + l);
+            }
         }
     }
     return "";

@@ -28,13 +28,12 @@ constexpr int kMaxRowDegree = 58;   // sign bits that fit the packed row state
 constexpr int kRefShift = 6;
 
 // Static work schedule of the row-parallel kernel (kernels.hip, k_decode_rows):
-// one thread per check row (thread t = row t) and CPT bit-node slots per
-// thread (slot s = t + threads*i). Slots are the columns sorted by degree
-// (stable), so each 64-slot wave group has a near-uniform degree; the c2v
-// message of bit-node slot s, edge kc (nlist order) lives at element
-//   gbase[s >> 6] + kc*64 + (s & 63)
-// of the per-codeword c2v array (e_pad elements), so a wave's bit-node reads
-// are 64 consecutive words (conflict-free LDS).
+// one thread per check row (thread t = row t) and up to CPT bit-node slots per
+// thread. Columns are sorted by degree (stable) and cut into 64-column groups
+// of near-uniform degree; edge kc (nlist order) of the group's column l lives
+// at c2v element gbase + kc*64 + l, so a wave's bit-node reads are 64
+// consecutive words (conflict-free LDS). Groups are assigned to waves by
+// longest-processing-time so the bit-node phase is balanced across waves.
 struct RowSchedule {
     int threads = 0, cpt = 0, dc = 0, e_pad = 0;
     std::vector<uint16_t> cn_cols;   // [threads * dc]  bit index of row edge k

@@ -38,6 +38,9 @@ template <> __device__ __forceinline__ double dinf<double>() { return __builtin_
 __device__ __forceinline__ float dabs(float x) { return __builtin_fabsf(x); }
 __device__ __forceinline__ double dabs(double x) { return __builtin_fabs(x); }
 __device__ __forceinline__ float dfloor(float x) { return __builtin_floorf(x); }
+// IEEE minNum: a NaN operand yields the other operand.
+__device__ __forceinline__ float dmin(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double dmin(double a, double b) { return __builtin_fmin(a, b); }
 __device__ __forceinline__ double dfloor(double x) { return __builtin_floor(x); }
 
 // sgn() of the reference (:518-523): x >= 0 -> +1 (so -0.0 -> +1, NaN -> -1).
@@ -345,12 +348,26 @@ __device__ __forceinline__ float nms_div<float>(float x, float alpha, const Deco
     return x / alpha;
 }
 
+// sum += c2v[base + k*64] for k in [k0, min(k0+K, gd)), loads issued first.
+template <typename F, int C, int K>
+__device__ __forceinline__ void vn_accumulate(const Pack<F, C> *c2v, int base, int gd, int k0, F (&sum)[C])
+{
+    Pack<F, C> r[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) r[j] = c2v[base + (k0 + j < gd ? k0 + j : k0) * 64];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        if (k0 + j < gd) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) sum[c] += r[j].v[c];
+        }
+}
+
 template <typename F, int SRC, int C, int DC, int CPT>
 __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, RowSched rs)
 {
     using MT = typename MetaOf<DC>::T;
     using P = Pack<F, C>;
-    constexpr MT NONE = (MT)((1u << MetaOf<DC>::SH) - 1u);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, nt = blockDim.x;
     const int N = g.N, EA = rs.e_pad + 64;         // + one dummy slot per lane for padding edges
@@ -468,38 +485,48 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
             for (int k = 0; k < DC; ++k) xin[k] = app[u16_at<DC>(colw, k)];   // padding edges read +INF
 #pragma unroll
             for (int c = 0; c < C; ++c) {
+                F ax[DC];
                 F mn1 = dinf<F>(), mn2 = dinf<F>();
-                MT amin = NONE, sg = 0;
+                MT sg = 0;
 #pragma unroll
                 for (int k = 0; k < DC; ++k) {
                     const F x = xin[k].v[c] - prev[c][k];                      // v2c (:469)
                     sg |= (MT)(!(x >= F(0))) << k;                              // sgn(v2c) (:518-523)
-                    const F ax = dabs(x);
-                    const bool le = ax <= mn1;                                  // :428-433
-                    const F m2c = (ax < mn2) ? ax : mn2;                        // :434-437
-                    mn2 = le ? mn1 : m2c;
-                    mn1 = le ? ax : mn1;
-                    amin = le ? (MT)k : amin;
+                    ax[k] = dabs(x);
+                    // :428-437 -- if (|x| <= m1) {m2 = m1; m1 = |x|} else if (|x| < m2) m2 = |x|
+                    // (NaN: no comparison holds and fmin returns the other operand).
+                    const bool le = ax[k] <= mn1;
+                    mn2 = dmin(mn2, le ? mn1 : ax[k]);
+                    mn1 = le ? ax[k] : mn1;
                 }
                 sg &= degmask;
-                MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask) : sg;   // prod*sgn(v2c_k)
-                F M1 = mn1, M2 = mn2;
-                if (a.variant == V_NMS) {
-                    M1 = nms_div<F>(mn1, alpha, a);
-                    M2 = nms_div<F>(mn2, alpha, a);
-                } else if (a.variant == V_OMS) {
+                const MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask) : sg;   // prod*sgn(v2c_k)
+                // The argmin edge gets m2, every other edge m1 (:444-447). |x_k| == m1
+                // identifies it: on a tie m2 == m1, so which tied edge is "argmin" does not matter.
+                if (a.variant != V_OMS) {
+                    F M1 = mn1, M2 = mn2;
+                    if (a.variant == V_NMS) {
+                        M1 = nms_div<F>(mn1, alpha, a);                         // :494-499
+                        M2 = nms_div<F>(mn2, alpha, a);
+                    }
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) {
+                        const F mag = (ax[k] == mn1) ? M2 : M1;
+                        prev[c][k] = ((eff >> k) & 1u) ? -mag : mag;
+                    }
+                } else {                                                        // :503-515
                     const F t1 = mn1 - delta, t2 = mn2 - delta;
                     const bool p1 = t1 > F(0), p2 = t2 > F(0);
-                    M1 = p1 ? t1 : F(0);
-                    M2 = p2 ? t2 : F(0);
-                    const MT abit = (amin < (MT)DC) ? ((MT)1 << amin) : (MT)0;
-                    if (!p1 || mn1 == F(0)) eff &= abit;
-                    if (!p2 || mn2 == F(0)) eff &= ~abit;
-                }
+                    const F M1 = p1 ? t1 : F(0), M2 = p2 ? t2 : F(0);
+                    // sgn(c2v) maps -0.0 to +1 and a zeroed message is +0
+                    const MT e1 = (!p1 || mn1 == F(0)) ? (MT)0 : eff;
+                    const MT e2 = (!p2 || mn2 == F(0)) ? (MT)0 : eff;
 #pragma unroll
-                for (int k = 0; k < DC; ++k) {
-                    const F mag = ((MT)k == amin) ? M2 : M1;
-                    prev[c][k] = ((eff >> k) & 1u) ? -mag : mag;
+                    for (int k = 0; k < DC; ++k) {
+                        const bool ism = ax[k] == mn1;
+                        const F mag = ism ? M2 : M1;
+                        prev[c][k] = (((ism ? e2 : e1) >> k) & 1u) ? -mag : mag;
+                    }
                 }
             }
 #pragma unroll
@@ -513,23 +540,20 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
             // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
 #pragma unroll
             for (int i = 0; i < CPT; ++i) {
+                const int gd = __builtin_amdgcn_readfirstlane((int)(vinfo[i] >> 24));   // wave-uniform
+                if (gd == 0) continue;
                 const int v = vcol[i];
                 const int base = (int)(vinfo[i] & 0xffffu);
-                const int gd = __builtin_amdgcn_readfirstlane((int)(vinfo[i] >> 24));   // wave-uniform
                 F sum[C];
 #pragma unroll
                 for (int c = 0; c < C; ++c) sum[c] = yq[c][i];
-                for (int k0 = 0; k0 < gd; k0 += 4) {   // 4 reads in flight; edges beyond a bit's degree hold +0
-                    P r[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) r[j] = c2v[base + (k0 + j < gd ? k0 + j : k0) * 64];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        if (k0 + j < gd) {
-#pragma unroll
-                            for (int c = 0; c < C; ++c) sum[c] += r[j].v[c];
-                        }
-                }
+                // all of a slot's reads in flight before the first add; edges past a
+                // bit's own degree hold +0
+                if (gd <= 4) vn_accumulate<F, C, 4>(c2v, base, gd, 0, sum);
+                else if (gd <= 8) vn_accumulate<F, C, 8>(c2v, base, gd, 0, sum);
+                else if (gd <= 12) vn_accumulate<F, C, 12>(c2v, base, gd, 0, sum);
+                else
+                    for (int k0 = 0; k0 < gd; k0 += 8) vn_accumulate<F, C, 8>(c2v, base, gd, k0, sum);
                 if (v >= 0) {
                     P o;
 #pragma unroll

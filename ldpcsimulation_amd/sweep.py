@@ -1,0 +1,109 @@
+"""SNR sweep on one or more GPUs -- replacement of the reference's sweep scripts.
+
+The reference launches one background process per SNR point, each appending
+one line to a shared log (C_implementations/scripts/minsum_example_*.sh:23-27,
+decodeMinSum.cpp:313-329). Here every SNR point runs on all ranks at once: the
+frames of a point are sharded over the GPUs by global frame index (one process
+per GPU, torch.distributed over RCCL, launched with torchrun), the six error
+counters are all-reduced per round, and rank 0 appends the reference's log
+line for each point.
+
+    python -m ldpcsimulation_amd.sweep ALIST --rate 0.5 --snr 1.0 1.25 1.5 -T 50 \\
+        --variant nms --alpha 1.25 --log results.txt
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m ldpcsimulation_amd.sweep ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+from . import native, sim
+
+VARIANTS = {"ms": native.MS, "nms": native.NMS, "oms": native.OMS}
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("alist")
+    p.add_argument("--rate", type=float, required=True)
+    p.add_argument("--snr", type=float, nargs="+", required=True, help="Eb/N0 points in dB")
+    p.add_argument("-T", "--iterations", type=int, default=10)
+    p.add_argument("--variant", choices=list(VARIANTS), default="ms")
+    p.add_argument("--alpha", type=float, default=1.0)
+    p.add_argument("--delta", type=float, default=0.0)
+    p.add_argument("--quantize", nargs=2, metavar=("YMAX", "Q"), help="-D quantizeSamples front-end")
+    p.add_argument("--saturate", type=float, metavar="YMAX", help="-D saturateSamples front-end")
+    p.add_argument("--precision", choices=["f32", "f64"], default="f32")
+    p.add_argument("--batch", type=int, default=65536, help="frames per GPU per round")
+    p.add_argument("--seed", type=int, default=None, help="noise seed (default: time)")
+    p.add_argument("--min-bit-errors", type=int, default=200)
+    p.add_argument("--min-frame-errors", type=int, default=40)
+    p.add_argument("--max-frames", type=int, default=None)
+    p.add_argument("--codewords", help="codeword file ('0'/'1' lines), as the reference's optional argument")
+    p.add_argument("--log", help="append the reference's tab-separated result line per point")
+    p.add_argument("--json", action="store_true", help="also print one JSON object per point")
+    return p.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = local if world > 1 else 0
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(device)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+    seed = a.seed if a.seed is not None else int(time.time())
+    cfg = native.DecoderConfig(variant=VARIANTS[a.variant], T=a.iterations, alpha=a.alpha, delta=a.delta,
+                               precision=native.F64 if a.precision == "f64" else native.F32)
+    extra = []
+    if a.quantize:
+        cfg.quantize, cfg.ymax, cfg.qbits = True, float(a.quantize[0]), int(a.quantize[1])
+        extra.append(cfg.ymax)
+    elif a.saturate is not None:
+        cfg.saturate, cfg.ymax = True, a.saturate
+        extra.append(cfg.ymax)
+    if a.variant == "nms":
+        extra.append(a.alpha)
+    elif a.variant == "oms":
+        extra.append(a.delta)
+    g = native.Graph.from_alist(a.alist)
+    ctx = native.Context(g, device, a.batch)
+    if a.codewords:
+        lines = [l.strip() for l in open(a.codewords) if l.strip()]
+        import numpy as np
+        ctx.set_codewords(np.array([[1 if ch == "1" else 0 for ch in l[:g.N]] for l in lines], dtype=np.uint8))
+    for k, snr in enumerate(a.snr):
+        def run_batch(first, n, snr=snr, k=k):
+            fr, _ = ctx.sim_batch(snr, a.rate, cfg, seed, k, first, n)
+            return fr
+        t0 = time.perf_counter()
+        res = sim.simulate_point(run_batch, g.N, a.iterations, snr, a.batch, a.min_bit_errors,
+                                 a.min_frame_errors, a.max_frames, device=device)
+        dt = time.perf_counter() - t0
+        if rank == 0:
+            line = res.log_line(a.alist, extra)
+            if a.log:
+                with open(a.log, "a") as f:
+                    f.write(line + "\n")
+            print(line, flush=True)
+            if a.json:
+                c = res.counts
+                print(json.dumps({"ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "seconds": dt,
+                                  "mbit_s": c["frames"] * g.N / dt / 1e6 if dt > 0 else None,
+                                  "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"])}),
+                      flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

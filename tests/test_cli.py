@@ -49,3 +49,20 @@ def test_cli_philox_mode_runs(tmp_path):
     assert "Final result:" in p.stdout
     fields = log.read_text().split("\t")
     assert fields[0] == "1.25" and fields[4] == "50" and fields[5] == "1.25"
+
+
+def test_sweep_driver_log_lines(tmp_path):
+    """ldpcsimulation_amd.sweep: one reference-format log line per SNR point."""
+    import sys
+    log = tmp_path / "sweep.txt"
+    p = subprocess.run([sys.executable, "-m", "ldpcsimulation_amd.sweep", code_path("80211n_1944_r12.alist"),
+                        "--rate", "0.5", "--snr", "1.0", "1.5", "-T", "50", "--variant", "nms", "--alpha", "1.25",
+                        "--batch", "8192", "--seed", "5", "--log", str(log), "--json"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr
+    lines = log.read_text().splitlines()
+    assert len(lines) == 2
+    f = lines[0].split("\t")
+    assert f[0] == "1" and f[4] == "50" and f[5] == "1.25" and f[6].endswith("80211n_1944_r12.alist")
+    fer = [float(l.split("\t")[3]) for l in lines]
+    assert 0.25 < fer[0] < 0.6 and 0.005 < fer[1] < 0.04     # SURVEY §6 reference FER 0.417 / 0.0181

@@ -1,0 +1,113 @@
+"""The SNR-point driver without a GPU: the reference's stop rule applied exactly,
+independent of batch size and of the number of ranks (gloo, world_size 2).
+
+Frame outcomes come from a deterministic fake keyed by the global frame index,
+standing in for ldpc_sim_batch (which is keyed the same way on the device)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from ldpcsimulation_amd import sim
+from ldpcsimulation_amd.native import FRAME_DTYPE
+
+N, T = 1944, 50
+
+
+def fake_frames(first, n):
+    f = np.arange(first, first + n, dtype=np.int64)
+    h = (f * 2654435761) & 0xFFFFFFFF
+    w = np.where((h >> 7) % 97 < 6, (h % 23) + 1, 0)
+    out = np.zeros(n, dtype=FRAME_DTYPE)
+    out["bit_err"] = w
+    out["uncoded_bit_err"] = (h >> 3) % 211
+    out["syndrome_fail"] = ((w > 0) & (f % 3 == 0)).astype(np.int32)
+    return out
+
+
+def sequential(min_bit=200, min_frame=40, max_frames=None):
+    """Frame-by-frame loop of decodeMinSum.cpp:189-288 on the fake outcomes."""
+    acc = np.zeros(6, dtype=np.int64)
+    hist = np.zeros(N, dtype=np.int64)
+    f = 0
+    while acc[0] < min_bit or acc[1] < min_frame:
+        if max_frames is not None and acc[3] >= max_frames:
+            break
+        r = fake_frames(f, 1)[0]
+        w = int(r["bit_err"])
+        acc += (w, w > 0, r["uncoded_bit_err"], 1, T, r["syndrome_fail"])
+        if w:
+            hist[w - 1] += 1
+        f += 1
+    return dict(zip(sim.COUNT_KEYS, (int(x) for x in acc))), hist
+
+
+@pytest.mark.parametrize("batch", [1, 7, 64, 1000, 5000])
+def test_exact_stop_independent_of_batch(batch):
+    want, hist = sequential()
+    res = sim.simulate_point(fake_frames, N, T, 1.5, batch)
+    assert res.counts == want
+    assert np.array_equal(res.hist, hist)
+
+
+def test_stop_rule_needs_both_thresholds():
+    assert not sim.stop_reached(199, 100)
+    assert not sim.stop_reached(1000, 39)
+    assert sim.stop_reached(200, 40)
+
+
+def test_max_frames_cap():
+    want, _ = sequential(min_bit=10 ** 9, min_frame=10 ** 9, max_frames=777)
+    res = sim.simulate_point(fake_frames, N, T, 1.5, 100, min_bit_err=10 ** 9, min_frame_err=10 ** 9,
+                             max_frames=777)
+    assert res.counts == want and res.counts["frames"] == 777
+
+
+def test_log_line_format():
+    r = sim.PointResult(1.5, 1008, 10, {"bit_err": 1715, "frame_err": 40, "uncoded_bit_err": 0,
+                                        "frames": 63, "iters": 630, "syndrome_fail": 0})
+    # the reference's own line for this run: "2\t0.0270062\t10\t0.634921\t10\t<alist>"
+    assert r.log_line("x.alist") == "1.5\t0.0270062\t10\t0.634921\t10\tx.alist"
+
+
+def test_wilson_and_z():
+    lo, hi = sim.wilson_interval(40, 2212)
+    assert lo < 40 / 2212 < hi
+    assert abs(sim.two_proportion_z(40, 2212, 40, 2212)) < 1e-12
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, batch, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = sim.simulate_point(fake_frames, N, T, 1.5, batch)
+        q.put((rank, res.counts, res.hist.tolist(), res.rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("batch", [16, 300])
+def test_two_ranks_gloo_identical_to_sequential(batch):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, batch, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want, hist = sequential()
+    for rank, counts, h, rounds in out:
+        assert counts == want, rank
+        assert np.array_equal(np.array(h), hist)
