@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <new>
 #include <string>
 #include <vector>
@@ -240,15 +241,24 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
 
     // Row-parallel schedule (the throughput kernel) when the graph fits it.
     {
-        int threads = ((g->M + 63) / 64) * 64;
+        // Two rows per thread in 512-thread blocks when M > 512 (two blocks per
+        // CU: their barriers overlap); LDPC_RPT=1|2 overrides (experiments).
+        // Rows per thread: 1 up to 512 rows (512-thread blocks), 2 up to 1024 rows
+        // (512 threads, two blocks per CU: measured 1.13x over one 1024-thread
+        // block with 1 row per thread on the N=1944 code); LDPC_RPT=1|2 overrides.
+        int rpt = g->M <= 512 ? 1 : 2;
+        if (const char *er = std::getenv("LDPC_RPT")) rpt = std::max(1, std::min(2, std::atoi(er)));
+        int threads = ((((g->M + rpt - 1) / rpt) + 63) / 64) * 64;
         if (threads < 64) threads = 64;
         int dc = 0, cpt = 0;
         for (int d : ldpc::kRowsDc)
             if (!dc && g->maxdc <= d) dc = d;
-        for (int q : ldpc::kRowsCpt)
-            if (!cpt && (long)threads * q >= g->N) cpt = q;
+        static const int cpt_for_rpt[][3] = {{0, 0, 0}, {2, 4, 0}, {4, 0, 0}};
+        for (int q : cpt_for_rpt[rpt])
+            if (q && !cpt && (long)(threads / 64) * q >= (g->N + 63) / 64) cpt = q;
         ldpc::RowSchedule hs;
-        if (threads <= ldpc::kRowsMaxThreads && dc && cpt && ldpc::build_row_schedule(*g, threads, cpt, dc, hs).empty()) {
+        if (threads <= ldpc::kRowsMaxThreadsForRpt[rpt] && dc && cpt &&
+            ldpc::build_row_schedule(*g, threads, cpt, dc, rpt, hs).empty()) {
             const size_t b_cc = al(2 * hs.cn_cols.size()), b_cp = al(2 * hs.cn_pos.size()), b_cd = al(hs.cn_deg.size()),
                          b_vc = al(2 * hs.vn_col.size()), b_vi = al(4 * hs.vn_info.size());
             CTX_TRY(c->sched.ensure(b_cc + b_cp + b_cd + b_vc + b_vi));
@@ -263,6 +273,7 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
             c->rs.cpt = hs.cpt;
             c->rs.dc = hs.dc;
             c->rs.e_pad = hs.e_pad;
+            c->rs.rpt = hs.rpt;
             c->rs.cn_cols = (const uint16_t *)sb;
             c->rs.cn_pos = (const uint16_t *)(sb + b_cc);
             c->rs.cn_deg = (const uint8_t *)(sb + b_cc + b_cp);

@@ -88,9 +88,9 @@ std::string build_graph(int N, int M, const int *num_nlist, const int *const *nl
     return "";
 }
 
-std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, RowSchedule &s)
+std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, int rpt, RowSchedule &s)
 {
-    if (threads % 64 || threads < g.M) return "rows exceed threads";
+    if (threads % 64 || (long)threads * rpt < g.M) return "rows exceed threads";
     if ((long)threads * cpt < g.N) return "bits exceed slots";
     if (g.maxdc > dc) return "row degree exceeds kernel bound";
     if (g.N > 65534) return "N exceeds 16-bit schedule";
@@ -98,6 +98,8 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
     s.threads = threads;
     s.cpt = cpt;
     s.dc = dc;
+    s.rpt = rpt;
+    const int rows = threads * rpt;
     // Stable sort of columns by decreasing degree -> slot order.
     std::vector<int> order(g.N);
     for (int i = 0; i < g.N; ++i) order[i] = i;
@@ -133,10 +135,10 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
     }
     s.vn_col.assign(nslots, 0xffff);
     s.vn_info.assign(nslots, 0);   // unused positions: group degree 0 (skipped)
-    s.cn_cols.assign((size_t)threads * dc, 0);
-    s.cn_pos.assign((size_t)threads * dc, 0);
-    s.cn_deg.assign(threads, 0);
-    for (int t = 0; t < threads; ++t)   // padding edges: read the +INF sentinel bit N, write the lane's dummy slot
+    s.cn_cols.assign((size_t)rows * dc, 0);
+    s.cn_pos.assign((size_t)rows * dc, 0);
+    s.cn_deg.assign(rows, 0);
+    for (int t = 0; t < rows; ++t)   // padding edges: read the +INF sentinel bit N, write the lane's dummy slot
         for (int k = 0; k < dc; ++k) {
             s.cn_cols[(size_t)t * dc + k] = (uint16_t)g.N;
             s.cn_pos[(size_t)t * dc + k] = (uint16_t)(s.e_pad + (t & 63));

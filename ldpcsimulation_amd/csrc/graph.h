@@ -28,17 +28,17 @@ constexpr int kMaxRowDegree = 58;   // sign bits that fit the packed row state
 constexpr int kRefShift = 6;
 
 // Static work schedule of the row-parallel kernel (kernels.hip, k_decode_rows):
-// one thread per check row (thread t = row t) and up to CPT bit-node slots per
-// thread. Columns are sorted by degree (stable) and cut into 64-column groups
+// RPT check rows per thread (thread t owns rows t, t + threads, ...) and up to
+// CPT bit-node slots per thread. Columns are sorted by degree (stable) and cut into 64-column groups
 // of near-uniform degree; edge kc (nlist order) of the group's column l lives
 // at c2v element gbase + kc*64 + l, so a wave's bit-node reads are 64
 // consecutive words (conflict-free LDS). Groups are assigned to waves by
 // longest-processing-time so the bit-node phase is balanced across waves.
 struct RowSchedule {
-    int threads = 0, cpt = 0, dc = 0, e_pad = 0;
-    std::vector<uint16_t> cn_cols;   // [threads * dc]  bit index of row edge k
-    std::vector<uint16_t> cn_pos;    // [threads * dc]  c2v element of row edge k
-    std::vector<uint8_t> cn_deg;     // [threads]
+    int threads = 0, cpt = 0, dc = 0, e_pad = 0, rpt = 1;
+    std::vector<uint16_t> cn_cols;   // [threads * rpt * dc]  bit index of edge k of row j
+    std::vector<uint16_t> cn_pos;    // [threads * rpt * dc]  c2v element of edge k of row j
+    std::vector<uint8_t> cn_deg;     // [threads * rpt]       (row j -> thread j % threads)
     std::vector<uint16_t> vn_col;    // [threads * cpt] column of slot s (0xffff = none)
     std::vector<uint32_t> vn_info;   // [threads * cpt] (gbase+lane) | deg << 16 | group degree << 24
 };
@@ -52,5 +52,5 @@ std::string load_alist(const char *path, ldpc_graph &g);
 // Row schedule for `threads` threads (multiple of 64, >= M), `cpt` bit slots
 // per thread (threads*cpt >= N) and row-degree bound dc. Returns "" or why the
 // graph does not fit (the caller then uses the generic kernel).
-std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, RowSchedule &s);
+std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, int rpt, RowSchedule &s);
 }  // namespace ldpc

@@ -39,10 +39,10 @@ struct DecodeArgs {
 
 // Device copy of graph.h's RowSchedule (row-parallel kernel).
 struct RowSched {
-    int threads, cpt, dc, e_pad;
-    const uint16_t *cn_cols;        // [threads * dc]
-    const uint16_t *cn_pos;         // [threads * dc]
-    const uint8_t *cn_deg;          // [threads]
+    int threads, cpt, dc, e_pad, rpt;
+    const uint16_t *cn_cols;        // [threads * rpt * dc]  (row j = thread j % threads, r = j / threads)
+    const uint16_t *cn_pos;         // [threads * rpt * dc]
+    const uint8_t *cn_deg;          // [threads * rpt]
     const uint16_t *vn_col;         // [threads * cpt]
     const uint32_t *vn_info;        // [threads * cpt]
 };
@@ -73,7 +73,9 @@ hipError_t verify_div_by_reciprocal(float alpha, float rcp, unsigned long long *
 
 // Row-kernel template bounds (host picks the smallest that fits).
 constexpr int kRowsMaxThreads = 1024;
-constexpr int kRowsCpt[] = {2, 4};
+constexpr int kRowsCpt[] = {2, 4, 8};
+// rows per thread -> block threads cap
+constexpr int kRowsMaxThreadsForRpt[] = {0, 1024, 512, 384};
 constexpr int kRowsDc[] = {8, 16, 32};
 
 }  // namespace ldpc

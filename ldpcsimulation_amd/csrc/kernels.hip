@@ -363,8 +363,17 @@ __device__ __forceinline__ void vn_accumulate(const Pack<F, C> *c2v, int base, i
         }
 }
 
-template <typename F, int SRC, int C, int DC, int CPT>
-__global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, RowSched rs)
+// Block shape per rows-per-thread: RPT=1 up to 1024 threads (4 waves/SIMD);
+// RPT=2 512 threads and RPT=3 384 threads, sized for two blocks per CU
+// (4 resp. 3 waves per SIMD: 128 resp. 168 VGPRs).
+template <int RPT> struct RowsShape;
+template <> struct RowsShape<1> { static constexpr int threads = 1024, waves_per_eu = 4; };
+template <> struct RowsShape<2> { static constexpr int threads = 512, waves_per_eu = 4; };
+template <> struct RowsShape<3> { static constexpr int threads = 384, waves_per_eu = 3; };
+
+template <typename F, int SRC, int C, int DC, int CPT, int RPT>
+__global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_eu) void k_decode_rows(
+    DecodeArgs a, DevGraph g, RowSched rs)
 {
     using MT = typename MetaOf<DC>::T;
     using P = Pack<F, C>;
@@ -375,16 +384,22 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
     P *c2v = app + (N + 2);                        // [EA] (N+2 keeps 16-B alignment)
     int *red = reinterpret_cast<int *>(c2v + EA);
 
-    // ---- the thread's share of the graph, in registers for the whole launch ----
-    const int deg = rs.cn_deg[tid];
-    const MT degmask = (deg >= (int)(8 * sizeof(MT))) ? ~(MT)0 : (((MT)1 << deg) - 1);
-    uint32_t colw[DC / 2], posw[DC / 2];
+    // ---- the thread's rows (tid + r*nt) and bit slots, in registers for the whole launch ----
+    int deg[RPT];
+    MT degmask[RPT];
+    uint32_t colw[RPT][DC / 2], posw[RPT][DC / 2];
 #pragma unroll
-    for (int q = 0; q < DC / 8; ++q) {
-        const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)tid * DC)[q];
-        const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)tid * DC)[q];
-        colw[4 * q + 0] = xc.x; colw[4 * q + 1] = xc.y; colw[4 * q + 2] = xc.z; colw[4 * q + 3] = xc.w;
-        posw[4 * q + 0] = xp.x; posw[4 * q + 1] = xp.y; posw[4 * q + 2] = xp.z; posw[4 * q + 3] = xp.w;
+    for (int r = 0; r < RPT; ++r) {
+        const int j = tid + r * nt;
+        deg[r] = rs.cn_deg[j];
+        degmask[r] = (deg[r] >= (int)(8 * sizeof(MT))) ? ~(MT)0 : (((MT)1 << deg[r]) - 1);
+#pragma unroll
+        for (int q = 0; q < DC / 8; ++q) {
+            const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)j * DC)[q];
+            const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)j * DC)[q];
+            colw[r][4 * q + 0] = xc.x; colw[r][4 * q + 1] = xc.y; colw[r][4 * q + 2] = xc.z; colw[r][4 * q + 3] = xc.w;
+            posw[r][4 * q + 0] = xp.x; posw[r][4 * q + 1] = xp.y; posw[r][4 * q + 2] = xp.z; posw[r][4 * q + 3] = xp.w;
+        }
     }
     int vcol[CPT];
     uint32_t vinfo[CPT];
@@ -471,70 +486,99 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
             for (int k = dg; k < gd; ++k) c2v[base + k * 64] = z;
         }
 
-        // c2v sent on each edge last iteration (the check node's own copy): +0 before the first.
-        F prev[C][DC];
+        // c2v sent on each edge last iteration: +0 before the first. RPT <= 2 keeps
+        // the check node's own copy in registers; larger RPT re-reads it from its
+        // c2v slots (written only by this thread, read by the bit phase) to stay
+        // within the register budget of two blocks per CU.
+        constexpr bool PREV_REG = RPT <= 2;
+        F prev[PREV_REG ? RPT : 1][C][DC];
 #pragma unroll
-        for (int c = 0; c < C; ++c)
+        for (int r = 0; r < RPT; ++r) {
+            if (PREV_REG) {
 #pragma unroll
-            for (int k = 0; k < DC; ++k) prev[c][k] = F(0);
+                for (int c = 0; c < C; ++c)
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) prev[PREV_REG ? r : 0][c][k] = F(0);
+            } else {
+                P z;
+#pragma unroll
+                for (int c = 0; c < C; ++c) z.v[c] = F(0);
+#pragma unroll
+                for (int k = 0; k < DC; ++k) c2v[u16_at<DC>(posw[r], k)] = z;
+            }
+        }
 
         for (int it = 0; it < a.T; ++it) {
             // ---- check nodes (:410-450, :494-515) ----
-            P xin[DC];
 #pragma unroll
-            for (int k = 0; k < DC; ++k) xin[k] = app[u16_at<DC>(colw, k)];   // padding edges read +INF
+            for (int r = 0; r < RPT; ++r) {
+                P xin[DC];
 #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                F ax[DC];
-                F mn1 = dinf<F>(), mn2 = dinf<F>();
-                MT sg = 0;
-#pragma unroll
-                for (int k = 0; k < DC; ++k) {
-                    const F x = xin[k].v[c] - prev[c][k];                      // v2c (:469)
-                    sg |= (MT)(!(x >= F(0))) << k;                              // sgn(v2c) (:518-523)
-                    ax[k] = dabs(x);
-                    // :428-437 -- if (|x| <= m1) {m2 = m1; m1 = |x|} else if (|x| < m2) m2 = |x|
-                    // (NaN: no comparison holds and fmin returns the other operand).
-                    const bool le = ax[k] <= mn1;
-                    mn2 = dmin(mn2, le ? mn1 : ax[k]);
-                    mn1 = le ? ax[k] : mn1;
-                }
-                sg &= degmask;
-                const MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask) : sg;   // prod*sgn(v2c_k)
-                // The argmin edge gets m2, every other edge m1 (:444-447). |x_k| == m1
-                // identifies it: on a tie m2 == m1, so which tied edge is "argmin" does not matter.
-                if (a.variant != V_OMS) {
-                    F M1 = mn1, M2 = mn2;
-                    if (a.variant == V_NMS) {
-                        M1 = nms_div<F>(mn1, alpha, a);                         // :494-499
-                        M2 = nms_div<F>(mn2, alpha, a);
-                    }
+                for (int k = 0; k < DC; ++k) xin[k] = app[u16_at<DC>(colw[r], k)];   // padding edges read +INF
+                F (&pv)[C][DC] = prev[PREV_REG ? r : 0];
+                if (!PREV_REG) {
 #pragma unroll
                     for (int k = 0; k < DC; ++k) {
-                        const F mag = (ax[k] == mn1) ? M2 : M1;
-                        prev[c][k] = ((eff >> k) & 1u) ? -mag : mag;
-                    }
-                } else {                                                        // :503-515
-                    const F t1 = mn1 - delta, t2 = mn2 - delta;
-                    const bool p1 = t1 > F(0), p2 = t2 > F(0);
-                    const F M1 = p1 ? t1 : F(0), M2 = p2 ? t2 : F(0);
-                    // sgn(c2v) maps -0.0 to +1 and a zeroed message is +0
-                    const MT e1 = (!p1 || mn1 == F(0)) ? (MT)0 : eff;
-                    const MT e2 = (!p2 || mn2 == F(0)) ? (MT)0 : eff;
+                        const P o = c2v[u16_at<DC>(posw[r], k)];
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) {
-                        const bool ism = ax[k] == mn1;
-                        const F mag = ism ? M2 : M1;
-                        prev[c][k] = (((ism ? e2 : e1) >> k) & 1u) ? -mag : mag;
+                        for (int c = 0; c < C; ++c) pv[c][k] = o.v[c];
                     }
                 }
-            }
 #pragma unroll
-            for (int k = 0; k < DC; ++k) {            // padding edges write the lane's dummy slot
-                P o;
+                for (int c = 0; c < C; ++c) {
+                    F ax[DC];
+                    F mn1 = dinf<F>(), mn2 = dinf<F>();
+                    MT sg = 0;
 #pragma unroll
-                for (int c = 0; c < C; ++c) o.v[c] = prev[c][k];
-                c2v[u16_at<DC>(posw, k)] = o;
+                    for (int k = 0; k < DC; ++k) {
+                        const F x = xin[k].v[c] - pv[c][k];                         // v2c (:469)
+                        sg |= (MT)(!(x >= F(0))) << k;                              // sgn(v2c) (:518-523)
+                        ax[k] = dabs(x);
+                        // :428-437 -- if (|x| <= m1) {m2 = m1; m1 = |x|} else if (|x| < m2) m2 = |x|
+                        // (NaN: no comparison holds and fmin returns the other operand).
+                        const bool le = ax[k] <= mn1;
+                        mn2 = dmin(mn2, le ? mn1 : ax[k]);
+                        mn1 = le ? ax[k] : mn1;
+                    }
+                    sg &= degmask[r];
+                    const MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask[r]) : sg;   // prod*sgn
+                    // The argmin edge gets m2, every other edge m1 (:444-447). |x_k| == m1
+                    // identifies it: on a tie m2 == m1, so which tied edge is "argmin" does not matter.
+                    if (a.variant != V_OMS) {
+                        F M1 = mn1, M2 = mn2;
+                        if (a.variant == V_NMS) {
+                            M1 = nms_div<F>(mn1, alpha, a);                     // :494-499
+                            M2 = nms_div<F>(mn2, alpha, a);
+                        }
+#pragma unroll
+                        for (int k = 0; k < DC; ++k) {
+                            const F mag = (ax[k] == mn1) ? M2 : M1;
+                            pv[c][k] = ((eff >> k) & 1u) ? -mag : mag;
+                        }
+                    } else {                                                    // :503-515
+                        const F t1 = mn1 - delta, t2 = mn2 - delta;
+                        const bool p1 = t1 > F(0), p2 = t2 > F(0);
+                        const F M1 = p1 ? t1 : F(0), M2 = p2 ? t2 : F(0);
+                        // sgn(c2v) maps -0.0 to +1 and a zeroed message is +0
+                        const MT e1 = (!p1 || mn1 == F(0)) ? (MT)0 : eff;
+                        const MT e2 = (!p2 || mn2 == F(0)) ? (MT)0 : eff;
+#pragma unroll
+                        for (int k = 0; k < DC; ++k) {
+                            const bool ism = ax[k] == mn1;
+                            const F mag = ism ? M2 : M1;
+                            pv[c][k] = (((ism ? e2 : e1) >> k) & 1u) ? -mag : mag;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {            // padding edges write the lane's dummy slot
+                    P o;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) o.v[c] = pv[c][k];
+                    c2v[u16_at<DC>(posw[r], k)] = o;
+                }
+                // keep the rows' live ranges apart (register pressure: two blocks per CU)
+                if (RPT > 1) __builtin_amdgcn_sched_barrier(0);
             }
             __syncthreads();
             // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
@@ -581,11 +625,14 @@ __global__ __launch_bounds__(1024) void k_decode_rows(DecodeArgs a, DevGraph g, 
                         if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
                     }
                 }
-                int par = 0;
 #pragma unroll
-                for (int k = 0; k < DC; ++k)
-                    if (k < deg) par ^= (app[u16_at<DC>(colw, k)].v[c] > F(0)) ? 0 : 1;
-                synd = par;
+                for (int r = 0; r < RPT; ++r) {
+                    int par = 0;
+#pragma unroll
+                    for (int k = 0; k < DC; ++k)
+                        if (k < deg[r]) par ^= (app[u16_at<DC>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
+                    synd |= par;
+                }
             }
             w = block_sum(w, red);
             const int uc = block_sum(unc[c], red);
@@ -701,11 +748,11 @@ static hipError_t launch_t(const DevGraph &g, const DecodeArgs &a, const KernelC
 }
 
 // Row kernel: dispatch on (C, DC, CPT). Persistent grid of the resident blocks.
-template <typename F, int SRC, int C, int DC, int CPT>
+template <typename F, int SRC, int C, int DC, int CPT, int RPT>
 static hipError_t launch_rows_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, const KernelChoice &kc,
                                 hipStream_t s, int num_cus)
 {
-    auto fn = k_decode_rows<F, SRC, C, DC, CPT>;
+    auto fn = k_decode_rows<F, SRC, C, DC, CPT, RPT>;
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, kc.lds_bytes);
     if (e != hipSuccess) return e;
     int per_cu = 0;
@@ -723,14 +770,18 @@ static hipError_t launch_rows_dc(const DevGraph &g, const RowSched &rs, const De
                                  hipStream_t s, int num_cus)
 {
     constexpr int C8 = sizeof(F) == 4 ? 2 : 1;
-#define LDPC_ROWS_CASE(CV, DCV, CPTV) \
-    if (rs.dc == DCV && rs.cpt == CPTV) return launch_rows_t<F, SRC, CV, DCV, CPTV>(g, rs, a, kc, s, num_cus);
-    LDPC_ROWS_CASE(C8, 8, 2)
-    LDPC_ROWS_CASE(C8, 8, 4)
-    LDPC_ROWS_CASE(1, 16, 2)
-    LDPC_ROWS_CASE(1, 16, 4)
-    LDPC_ROWS_CASE(1, 32, 2)
-    LDPC_ROWS_CASE(1, 32, 4)
+#define LDPC_ROWS_CASE(CV, DCV, CPTV, RPTV)                                   \
+    if (rs.dc == DCV && rs.cpt == CPTV && rs.rpt == RPTV)                   \
+        return launch_rows_t<F, SRC, CV, DCV, CPTV, RPTV>(g, rs, a, kc, s, num_cus);
+    LDPC_ROWS_CASE(C8, 8, 2, 1)
+    LDPC_ROWS_CASE(C8, 8, 4, 1)
+    LDPC_ROWS_CASE(C8, 8, 4, 2)
+    LDPC_ROWS_CASE(1, 16, 2, 1)
+    LDPC_ROWS_CASE(1, 16, 4, 1)
+    LDPC_ROWS_CASE(1, 16, 4, 2)
+    LDPC_ROWS_CASE(1, 32, 2, 1)
+    LDPC_ROWS_CASE(1, 32, 4, 1)
+    LDPC_ROWS_CASE(1, 32, 4, 2)
 #undef LDPC_ROWS_CASE
     return hipErrorInvalidValue;
 }
@@ -761,9 +812,10 @@ int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc)
     hipError_t e;
     if (kc.name[0] == 'r') {
         // the row kernels of one (C) share the LDS / thread shape
-        const void *fn = f64 ? (const void *)k_decode_rows<double, SRC_PHILOX, 1, 8, 2>
-                             : (kc.cw_per_block == 2 ? (const void *)k_decode_rows<float, SRC_PHILOX, 2, 8, 2>
-                                                     : (const void *)k_decode_rows<float, SRC_PHILOX, 1, 16, 2>);
+        // occupancy of a representative instantiation of the same block shape
+        const void *fn = f64 ? (const void *)k_decode_rows<double, SRC_PHILOX, 1, 8, 4, 2>
+                             : (kc.cw_per_block == 2 ? (const void *)k_decode_rows<float, SRC_PHILOX, 2, 8, 4, 2>
+                                                     : (const void *)k_decode_rows<float, SRC_PHILOX, 1, 16, 4, 2>);
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kc.lds_bytes);
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads, kc.lds_bytes);
     } else if (kc.lds_bytes > 0) {
