@@ -18,7 +18,19 @@ def pytest_configure(config):
 
 
 def code_path(name: str) -> str:
-    return os.path.join(CODES, name)
+    """Path of a code fixture; *.alist stored as *.alist.xz is decompressed once into .cache/."""
+    p = os.path.join(CODES, name)
+    if not os.path.exists(p) and os.path.exists(p + ".xz"):
+        import lzma
+        cache = os.path.join(CODES, ".cache")
+        os.makedirs(cache, exist_ok=True)
+        p = os.path.join(cache, name)
+        if not os.path.exists(p):
+            tmp = p + f".{os.getpid()}.tmp"
+            with lzma.open(os.path.join(CODES, name + ".xz"), "rb") as fi, open(tmp, "wb") as fo:
+                fo.write(fi.read())
+            os.replace(tmp, p)
+    return p
 
 
 def golden_runs():
