@@ -45,6 +45,14 @@ $(BINDIR)/decodeNormalizedMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
 $(BINDIR)/decodeOffsetMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
 	g++ $(CXXFLAGS) -D quantizeSamples -D offsetMS -o $@ $< $(CLI_LINK)
 
+# Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> lib/variants/libldpc_hip_x.so
+variant:
+	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/api.o $(CSRC)/api.cpp
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
+	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/graph.o
+
 oracle:
 	$(MAKE) -f oracle/Makefile
 
@@ -55,4 +63,4 @@ ref:
 clean:
 	rm -rf $(LIBDIR) $(BINDIR) oracle/liboracle.so
 
-.PHONY: all oracle ref clean
+.PHONY: all oracle ref clean variant

@@ -394,11 +394,35 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64)
         if (gblocks > a.batch) gblocks = a.batch;
         HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks));
     }
+#ifdef LDPC_STAMPS
+    // diagnostic builds: per-block phase cycle sums appended to $LDPC_STAMPS
+    static DevBuf stamp_buf;
+    ldpc::DecodeArgs as = a;
+    const char *stamp_path = std::getenv("LDPC_STAMPS");
+    if (stamp_path) {
+        HIP_TRY(stamp_buf.ensure(8192 * 4 * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(stamp_buf.p, 0, stamp_buf.n, c->stream));
+        as.stamps = (unsigned long long *)stamp_buf.p;
+    }
+#define a as
+#endif
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream, c->has_rs ? &c->rs : nullptr,
                                 c->num_cus));
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+#ifdef LDPC_STAMPS
+#undef a
+    if (stamp_path) {
+        std::vector<unsigned long long> h(8192 * 4);
+        HIP_TRY(hipMemcpyAsync(h.data(), stamp_buf.p, stamp_buf.n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (FILE *f = std::fopen(stamp_path, "ab")) {
+            std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+            std::fclose(f);
+        }
+    }
+#endif
     return LDPC_OK;
 }
 

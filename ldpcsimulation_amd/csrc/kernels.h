@@ -35,6 +35,7 @@ struct DecodeArgs {
     int4 *frame_res;                // [batch] {bit_err, uncoded, syndrome_fail, 0} or null
     unsigned long long *counts;     // [6] accumulated
     unsigned long long *hist;       // [N] accumulated (weight w -> hist[w-1])
+    unsigned long long *stamps;     // diagnostic builds (-DLDPC_STAMPS): [grid][4] cycle sums, else null
 };
 
 // Device copy of graph.h's RowSchedule (row-parallel kernel).

@@ -23,6 +23,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 namespace ldpc {
 
@@ -107,6 +108,13 @@ __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, double &n0,
     n0 = rad * c;
     n1 = rad * s;
 }
+
+// Diagnostic phase timing (-DLDPC_STAMPS builds only; never in the shipped kernel).
+#ifdef LDPC_STAMPS
+#define STAMP(var) unsigned long long var = (threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0ull
+#else
+#define STAMP(var) [[maybe_unused]] constexpr unsigned long long var = 0ull
+#endif
 
 // Sum over the workgroup (64-wide waves, <= 16 waves).
 __device__ __forceinline__ int block_sum(int x, int *red)
@@ -363,12 +371,128 @@ __device__ __forceinline__ void vn_accumulate(const Pack<F, C> *c2v, int base, i
         }
 }
 
+// Check node, exact path: the reference's comparisons for any input, incl.
+// infinities and NaN (checkNodeUpdates :410-450, applyNormalization :494-499,
+// applyOffset :503-515). pv[k].v[c]: in = c2v sent last iteration, out = new c2v.
+template <typename F, int C, int DC, typename MT>
+__device__ __forceinline__ void cn_exact(const Pack<F, C> (&xin)[DC], int c, Pack<F, C> (&pv)[DC], MT degmask,
+                                         const DecodeArgs &a, F alpha, F delta)
+{
+    F ax[DC];
+    F mn1 = dinf<F>(), mn2 = dinf<F>();
+    MT sg = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const F x = xin[k].v[c] - pv[k].v[c];                       // v2c (:469)
+        sg |= (MT)(!(x >= F(0))) << k;                              // sgn(v2c) (:518-523)
+        ax[k] = dabs(x);
+        // :428-437 -- if (|x| <= m1) {m2 = m1; m1 = |x|} else if (|x| < m2) m2 = |x|
+        // (NaN: no comparison holds and fmin returns the other operand).
+        const bool le = ax[k] <= mn1;
+        mn2 = dmin(mn2, le ? mn1 : ax[k]);
+        mn1 = le ? ax[k] : mn1;
+    }
+    sg &= degmask;
+    const MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask) : sg;   // prod*sgn(v2c_k)
+    // The argmin edge gets m2, every other edge m1 (:444-447). |x_k| == m1
+    // identifies it: on a tie m2 == m1, so which tied edge is "argmin" does not matter.
+    if (a.variant != V_OMS) {
+        F M1 = mn1, M2 = mn2;
+        if (a.variant == V_NMS) {
+            M1 = nms_div<F>(mn1, alpha, a);
+            M2 = nms_div<F>(mn2, alpha, a);
+        }
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const F mag = (ax[k] == mn1) ? M2 : M1;
+            pv[k].v[c] = ((eff >> k) & 1u) ? -mag : mag;
+        }
+    } else {
+        const F t1 = mn1 - delta, t2 = mn2 - delta;
+        const bool p1 = t1 > F(0), p2 = t2 > F(0);
+        const F M1 = p1 ? t1 : F(0), M2 = p2 ? t2 : F(0);
+        // sgn(c2v) maps -0.0 to +1 and a zeroed message is +0
+        const MT e1 = (!p1 || mn1 == F(0)) ? (MT)0 : eff;
+        const MT e2 = (!p2 || mn2 == F(0)) ? (MT)0 : eff;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const bool ism = ax[k] == mn1;
+            const F mag = ism ? M2 : M1;
+            pv[k].v[c] = (((ism ? e2 : e1) >> k) & 1u) ? -mag : mag;
+        }
+    }
+}
+
+// Check node, fast fp32 path (MS, and NMS with a verified reciprocal). Exact
+// whenever every c2v magnitude entering the iteration is below 1e30: then
+// every app and v2c is finite (|app| <= |yq| + 255*1e30 < FLT_MAX), no NaN
+// occurs, and
+//   m2' = med3(m1, |x|, m2), m1' = min(m1, |x|)
+// is exactly the reference's update (m1 <= m2 always). app is never -0 (yq is
+// canonicalised, see the kernel), so v2c = app - c2v is never -0 either and
+// its sign bit is the reference's sgn(v2c) (:518-523): the row parity is the
+// xor of the v2c bit patterns, and c2v_k = (m1|m2) with sign bit
+// parity ^ sign(v2c_k) (a zero magnitude keeps that sign, as prod*min*sgn
+// does). Padding edges read +inf: sign +, never below m2. The new messages
+// are always committed; the return value is false when one of them reaches
+// 1e30 (or is inf), and the caller hands the block to the exact path before
+// the next iteration (keeping the premise true).
+template <int DC, int C>
+__device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DC], Pack<float, C> (&pv)[DC], bool nms,
+                                        float alpha, float rcp)
+{
+    constexpr uint32_t SIGN = 0x80000000u;
+    Pack<float, C> x[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k)
+#pragma unroll
+        for (int c = 0; c < C; ++c) x[k].v[c] = xin[k].v[c] - pv[k].v[c];          // v2c (:469)
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        float mn1 = __builtin_huge_valf(), mn2 = __builtin_huge_valf();
+        uint32_t par = 0;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const float ax = __builtin_fabsf(x[k].v[c]);
+            mn2 = __builtin_amdgcn_fmed3f(mn1, ax, mn2);
+            mn1 = __builtin_fminf(mn1, ax);
+            par ^= __float_as_uint(x[k].v[c]);
+        }
+        float M1 = mn1, M2 = mn2;
+        if (nms) {   // x/alpha = q + (x - q*alpha)*r, q = x*r (verified for all finite x); inf/alpha = inf
+            const float q1 = mn1 * rcp, q2 = mn2 * rcp;
+            const float d1 = __builtin_fmaf(__builtin_fmaf(-q1, alpha, mn1), rcp, q1);
+            const float d2 = __builtin_fmaf(__builtin_fmaf(-q2, alpha, mn2), rcp, q2);
+            M1 = mn1 < __builtin_huge_valf() ? d1 : mn1;
+            M2 = mn2 < __builtin_huge_valf() ? d2 : mn2;
+        }
+        ok &= M2 < 1e30f;
+        const uint32_t s1 = __float_as_uint(M1) ^ (par & SIGN), s2 = __float_as_uint(M2) ^ (par & SIGN);
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const uint32_t m = (__builtin_fabsf(x[k].v[c]) == mn1) ? s2 : s1;
+            pv[k].v[c] = __uint_as_float(m ^ (__float_as_uint(x[k].v[c]) & SIGN));
+        }
+    }
+    return ok;
+}
+
+template <int DC, int C>
+__device__ __forceinline__ bool cn_fast(const Pack<double, C> (&)[DC], Pack<double, C> (&)[DC], bool, float, float)
+{
+    return false;   // never called: fp64 always takes the exact path
+}
+
 // Block shape per rows-per-thread: RPT=1 up to 1024 threads (4 waves/SIMD);
 // RPT=2 512 threads and RPT=3 384 threads, sized for two blocks per CU
 // (4 resp. 3 waves per SIMD: 128 resp. 168 VGPRs).
 template <int RPT> struct RowsShape;
 template <> struct RowsShape<1> { static constexpr int threads = 1024, waves_per_eu = 4; };
-template <> struct RowsShape<2> { static constexpr int threads = 512, waves_per_eu = 4; };
+#ifndef LDPC_RPT2_WAVES
+#define LDPC_RPT2_WAVES 4
+#endif
+template <> struct RowsShape<2> { static constexpr int threads = 512, waves_per_eu = LDPC_RPT2_WAVES; };
 template <> struct RowsShape<3> { static constexpr int threads = 384, waves_per_eu = 3; };
 
 template <typename F, int SRC, int C, int DC, int CPT, int RPT>
@@ -418,7 +542,10 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
 
     const F alpha = (F)a.alpha, delta = (F)a.delta;
     const int ngrp = (a.batch + C - 1) / C;
+    unsigned long long st_chan = 0, st_cn = 0, st_vn = 0, st_acct = 0;
+    (void)st_chan; (void)st_cn; (void)st_vn; (void)st_acct;
     for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+        STAMP(t_start);
         // ---- channel (:214-238), staged through the c2v area ----
         int unc[C];
         const int8_t *cvec[C];
@@ -469,10 +596,15 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
         for (int i = 0; i < CPT; ++i) {
             const int v = vcol[i];
             const P st = c2v[v >= 0 ? v : 0];
+            // yq + 0 maps -0 to +0, so app is never -0: v2c = app - c2v differs
+            // at most in the sign of a zero, which sgn() and |.| ignore, and
+            // the decision app > 0 is the same (the fast check node relies on it)
+            P q;
 #pragma unroll
-            for (int c = 0; c < C; ++c) yq[c][i] = st.v[c];
-            if (v >= 0) app[v] = st;   // v2c = yq on the first pass (:364-370)
+            for (int c = 0; c < C; ++c) q.v[c] = yq[c][i] = st.v[c] + F(0);
+            if (v >= 0) app[v] = q;   // v2c = yq on the first pass (:364-370)
         }
+        if (tid == 0) red[31] = 0;     // fast check-node path allowed
         __syncthreads();
         // Padding slots of the bit-node layout hold +0 (adding +0 leaves every
         // sum, and hence every decision, unchanged).
@@ -490,15 +622,17 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
         // the check node's own copy in registers; larger RPT re-reads it from its
         // c2v slots (written only by this thread, read by the bit phase) to stay
         // within the register budget of two blocks per CU.
+        // (Re-reading is only safe on the exact path: padding edges share per-lane
+        // dummy slots, so their "old message" is whatever another row wrote there.)
         constexpr bool PREV_REG = RPT <= 2;
-        F prev[PREV_REG ? RPT : 1][C][DC];
+        P prev[PREV_REG ? RPT : 1][DC];
 #pragma unroll
         for (int r = 0; r < RPT; ++r) {
             if (PREV_REG) {
 #pragma unroll
-                for (int c = 0; c < C; ++c)
+                for (int k = 0; k < DC; ++k)
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) prev[PREV_REG ? r : 0][c][k] = F(0);
+                    for (int c = 0; c < C; ++c) prev[PREV_REG ? r : 0][k].v[c] = F(0);
             } else {
                 P z;
 #pragma unroll
@@ -508,105 +642,88 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
             }
         }
 
-        for (int it = 0; it < a.T; ++it) {
-            // ---- check nodes (:410-450, :494-515) ----
+        STAMP(t_iter0);
+#ifdef LDPC_STAMPS
+        st_chan += t_iter0 - t_start;
+#endif
+        // One iteration loop, instantiated twice: the fast check-node loop runs
+        // while its premise holds (flag red[31] clear: every c2v entering the
+        // iteration is below 1e30) and hands over to the exact loop, which
+        // continues from the same state. Separate loops keep the two check-node
+        // bodies out of each other's register allocation.
+        auto iterate = [&](auto fast_tag, int it0) -> int {
+            constexpr bool FAST = decltype(fast_tag)::value;
+            int it = it0;
+            for (; it < a.T; ++it) {
+                STAMP(t_cn0);
+                if (FAST && __builtin_amdgcn_readfirstlane(red[31]) != 0) break;
+                // ---- check nodes (:410-450, :494-515) ----
 #pragma unroll
-            for (int r = 0; r < RPT; ++r) {
-                P xin[DC];
+                for (int r = 0; r < RPT; ++r) {
+                    P xin[DC];
 #pragma unroll
-                for (int k = 0; k < DC; ++k) xin[k] = app[u16_at<DC>(colw[r], k)];   // padding edges read +INF
-                F (&pv)[C][DC] = prev[PREV_REG ? r : 0];
-                if (!PREV_REG) {
+                    for (int k = 0; k < DC; ++k) xin[k] = app[u16_at<DC>(colw[r], k)];   // padding edges read +INF
+                    P (&pv)[DC] = prev[PREV_REG ? r : 0];
+                    if (!PREV_REG) {
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) {
-                        const P o = c2v[u16_at<DC>(posw[r], k)];
+                        for (int k = 0; k < DC; ++k) pv[k] = c2v[u16_at<DC>(posw[r], k)];
+                    }
+                    if constexpr (FAST) {
+                        const bool ok = cn_fast<DC, C>(xin, pv, a.variant == V_NMS, (float)alpha, a.alpha_rcp);
+                        // Rows past M (degree 0) only write the never-read dummy slots.
+                        if (!ok && deg[r] > 0) red[31] = 1;
+                    } else {
 #pragma unroll
-                        for (int c = 0; c < C; ++c) pv[c][k] = o.v[c];
+                        for (int c = 0; c < C; ++c) cn_exact<F, C, DC>(xin, c, pv, degmask[r], a, alpha, delta);
+                    }
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) c2v[u16_at<DC>(posw[r], k)] = pv[k];   // padding edges: the lane's dummy slot
+#ifndef LDPC_NO_ROW_FENCE
+                    // keep the rows' live ranges apart (register pressure: two blocks per CU)
+                    if (RPT > 1) __builtin_amdgcn_sched_barrier(0);
+#endif
+                }
+                __syncthreads();
+                STAMP(t_vn0);
+#ifdef LDPC_STAMPS
+                st_cn += t_vn0 - t_cn0;
+#endif
+                // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
+#pragma unroll
+                for (int i = 0; i < CPT; ++i) {
+                    const int gd = __builtin_amdgcn_readfirstlane((int)(vinfo[i] >> 24));   // wave-uniform
+                    if (gd == 0) continue;
+                    const int v = vcol[i];
+                    const int base = (int)(vinfo[i] & 0xffffu);
+                    F sum[C];
+#pragma unroll
+                    for (int c = 0; c < C; ++c) sum[c] = yq[c][i];
+                    // all of a slot's reads in flight before the first add; edges past a
+                    // bit's own degree hold +0
+                    if (gd <= 4) vn_accumulate<F, C, 4>(c2v, base, gd, 0, sum);
+                    else if (gd <= 8) vn_accumulate<F, C, 8>(c2v, base, gd, 0, sum);
+                    else if (gd <= 12) vn_accumulate<F, C, 12>(c2v, base, gd, 0, sum);
+                    else
+                        for (int k0 = 0; k0 < gd; k0 += 8) vn_accumulate<F, C, 8>(c2v, base, gd, k0, sum);
+                    if (v >= 0) {
+                        P o;
+#pragma unroll
+                        for (int c = 0; c < C; ++c) o.v[c] = sum[c];
+                        app[v] = o;
                     }
                 }
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    F ax[DC];
-                    F mn1 = dinf<F>(), mn2 = dinf<F>();
-                    MT sg = 0;
-#pragma unroll
-                    for (int k = 0; k < DC; ++k) {
-                        const F x = xin[k].v[c] - pv[c][k];                         // v2c (:469)
-                        sg |= (MT)(!(x >= F(0))) << k;                              // sgn(v2c) (:518-523)
-                        ax[k] = dabs(x);
-                        // :428-437 -- if (|x| <= m1) {m2 = m1; m1 = |x|} else if (|x| < m2) m2 = |x|
-                        // (NaN: no comparison holds and fmin returns the other operand).
-                        const bool le = ax[k] <= mn1;
-                        mn2 = dmin(mn2, le ? mn1 : ax[k]);
-                        mn1 = le ? ax[k] : mn1;
-                    }
-                    sg &= degmask[r];
-                    const MT eff = (__popcll((unsigned long long)sg) & 1) ? (sg ^ degmask[r]) : sg;   // prod*sgn
-                    // The argmin edge gets m2, every other edge m1 (:444-447). |x_k| == m1
-                    // identifies it: on a tie m2 == m1, so which tied edge is "argmin" does not matter.
-                    if (a.variant != V_OMS) {
-                        F M1 = mn1, M2 = mn2;
-                        if (a.variant == V_NMS) {
-                            M1 = nms_div<F>(mn1, alpha, a);                     // :494-499
-                            M2 = nms_div<F>(mn2, alpha, a);
-                        }
-#pragma unroll
-                        for (int k = 0; k < DC; ++k) {
-                            const F mag = (ax[k] == mn1) ? M2 : M1;
-                            pv[c][k] = ((eff >> k) & 1u) ? -mag : mag;
-                        }
-                    } else {                                                    // :503-515
-                        const F t1 = mn1 - delta, t2 = mn2 - delta;
-                        const bool p1 = t1 > F(0), p2 = t2 > F(0);
-                        const F M1 = p1 ? t1 : F(0), M2 = p2 ? t2 : F(0);
-                        // sgn(c2v) maps -0.0 to +1 and a zeroed message is +0
-                        const MT e1 = (!p1 || mn1 == F(0)) ? (MT)0 : eff;
-                        const MT e2 = (!p2 || mn2 == F(0)) ? (MT)0 : eff;
-#pragma unroll
-                        for (int k = 0; k < DC; ++k) {
-                            const bool ism = ax[k] == mn1;
-                            const F mag = ism ? M2 : M1;
-                            pv[c][k] = (((ism ? e2 : e1) >> k) & 1u) ? -mag : mag;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < DC; ++k) {            // padding edges write the lane's dummy slot
-                    P o;
-#pragma unroll
-                    for (int c = 0; c < C; ++c) o.v[c] = pv[c][k];
-                    c2v[u16_at<DC>(posw[r], k)] = o;
-                }
-                // keep the rows' live ranges apart (register pressure: two blocks per CU)
-                if (RPT > 1) __builtin_amdgcn_sched_barrier(0);
+                __syncthreads();
+#ifdef LDPC_STAMPS
+                { STAMP(t_vn1); st_vn += t_vn1 - t_vn0; }
+#endif
             }
-            __syncthreads();
-            // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
-#pragma unroll
-            for (int i = 0; i < CPT; ++i) {
-                const int gd = __builtin_amdgcn_readfirstlane((int)(vinfo[i] >> 24));   // wave-uniform
-                if (gd == 0) continue;
-                const int v = vcol[i];
-                const int base = (int)(vinfo[i] & 0xffffu);
-                F sum[C];
-#pragma unroll
-                for (int c = 0; c < C; ++c) sum[c] = yq[c][i];
-                // all of a slot's reads in flight before the first add; edges past a
-                // bit's own degree hold +0
-                if (gd <= 4) vn_accumulate<F, C, 4>(c2v, base, gd, 0, sum);
-                else if (gd <= 8) vn_accumulate<F, C, 8>(c2v, base, gd, 0, sum);
-                else if (gd <= 12) vn_accumulate<F, C, 12>(c2v, base, gd, 0, sum);
-                else
-                    for (int k0 = 0; k0 < gd; k0 += 8) vn_accumulate<F, C, 8>(c2v, base, gd, k0, sum);
-                if (v >= 0) {
-                    P o;
-#pragma unroll
-                    for (int c = 0; c < C; ++c) o.v[c] = sum[c];
-                    app[v] = o;
-                }
-            }
-            __syncthreads();
-        }
+            return it;
+        };
+        int it_done = 0;
+        if constexpr (sizeof(F) == 4 && PREV_REG)
+            if (a.variant == V_MS || (a.variant == V_NMS && a.nms_fast)) it_done = iterate(std::true_type{}, 0);
+        if (it_done < a.T) iterate(std::false_type{}, it_done);
+        STAMP(t_acct0);
 
         // ---- decisions, error weight, syndrome, accounting ----
 #pragma unroll
@@ -649,7 +766,18 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
             }
         }
         __syncthreads();
+#ifdef LDPC_STAMPS
+        { STAMP(t_end); st_acct += t_end - t_acct0; }
+#endif
     }
+#ifdef LDPC_STAMPS
+    if (tid == 0 && a.stamps) {
+        a.stamps[blockIdx.x * 4 + 0] = st_chan;
+        a.stamps[blockIdx.x * 4 + 1] = st_cn;
+        a.stamps[blockIdx.x * 4 + 2] = st_vn;
+        a.stamps[blockIdx.x * 4 + 3] = st_acct;
+    }
+#endif
 }
 
 // Exhaustive check of the reciprocal division (see kernels.h).
@@ -688,12 +816,20 @@ constexpr size_t kMaxLds = 160 * 1024;
 
 // Codewords per thread: 2 for the fp32 DC=8 kernel (no spills at 101 VGPRs),
 // 1 where two would spill (fp64, wider rows).
-static int rows_cw_per_block(bool f64, int dc) { return (!f64 && dc == 8) ? 2 : 1; }
+static int rows_cw_per_block(bool f64, int dc)
+{
+#ifdef LDPC_C1
+    (void)f64; (void)dc;
+    return 1;
+#else
+    return (!f64 && dc == 8) ? 2 : 1;
+#endif
+}
 
 static size_t rows_lds(const DevGraph &g, const RowSched &rs, bool f64, int C)
 {
     const size_t fs = f64 ? 8 : 4;
-    return ((size_t)C * ((size_t)g.N + 2 + (size_t)rs.e_pad + 64) * fs + 64 + 15) & ~(size_t)15;
+    return ((size_t)C * ((size_t)g.N + 2 + (size_t)rs.e_pad + 64) * fs + 128 + 15) & ~(size_t)15;
 }
 
 KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force)
@@ -769,7 +905,11 @@ template <typename F, int SRC>
 static hipError_t launch_rows_dc(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, const KernelChoice &kc,
                                  hipStream_t s, int num_cus)
 {
+#ifdef LDPC_C1
+    constexpr int C8 = 1;
+#else
     constexpr int C8 = sizeof(F) == 4 ? 2 : 1;
+#endif
 #define LDPC_ROWS_CASE(CV, DCV, CPTV, RPTV)                                   \
     if (rs.dc == DCV && rs.cpt == CPTV && rs.rpt == RPTV)                   \
         return launch_rows_t<F, SRC, CV, DCV, CPTV, RPTV>(g, rs, a, kc, s, num_cus);

@@ -14,6 +14,9 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "lib", "libldpc_hip.so")
+# A/B experiments: LDPC_LIB=<name> loads lib/variants/libldpc_hip_<name>.so (built by `make variant`)
+if os.environ.get("LDPC_LIB"):
+    LIB_PATH = os.path.join(_PKG, "lib", "variants", f"libldpc_hip_{os.environ['LDPC_LIB']}.so")
 
 LDPC_OK = 0
 MS, NMS, OMS = 0, 1, 2

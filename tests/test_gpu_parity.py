@@ -164,8 +164,10 @@ def test_all_kernels_bit_identical(monkeypatch, code):
             monkeypatch.setenv("LDPC_KERNEL", k)
         ctxs[k] = native.Context(g, 0, 300)
     monkeypatch.delenv("LDPC_KERNEL", raising=False)
-    cfg = native.DecoderConfig(variant=native.OMS, delta=0.1, T=15, quantize=True, ymax=1.5, qbits=5)
-    for prec in (native.F32, native.F64):
+    cfgs = [native.DecoderConfig(variant=native.OMS, delta=0.1, T=15, quantize=True, ymax=1.5, qbits=5),
+            native.DecoderConfig(variant=native.NMS, alpha=1.25, T=15),
+            native.DecoderConfig(variant=native.MS, T=15)]
+    for cfg, prec in ((c, p) for c in cfgs for p in (native.F32, native.F64)):
         cfg.precision = prec
         names = {k: c.kernel_info(cfg)["kernel"] for k, c in ctxs.items()}
         assert names["lds"] == "lds" and names["global"] == "global"
@@ -236,3 +238,52 @@ def test_fer_matches_reference_statistically(gpu_ctx_factory):
         _, cnt = ctx.sim_batch(ebn0, 0.5, cfg, seed=2026, stream_id=int(ebn0 * 100), first_cw=0, batch=16384)
         z = two_proportion_z(cnt.frame_err, cnt.frames, k_ref, n_ref)
         assert abs(z) < 3, (ebn0, cnt.frame_err, cnt.frames, z)
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("vname", ["ms", "nms"])
+def test_degree_one_check_infinities_exact(tmp_path, prec, vname):
+    """A degree-1 check sends +-inf (min2 of one edge, :419-447); the sums then hit
+    inf - inf = NaN. The fast fp32 check-node path must hand over to the exact path
+    so decisions still equal the oracle's (reference semantics for inf/NaN)."""
+    from ldpcsimulation_amd import codes
+    native = _native()
+    H = codes.read_alist(code_path("PEGReg504x1008.alist"))
+    rows = H.rows + [[5], [17, 900]]                     # add a degree-1 and a degree-2 check
+    H2 = codes.ParityCheck.from_rows(H.N, rows)
+    path = str(tmp_path / "peg_deg1.alist")
+    codes.write_alist(H2, path)
+    ctx = native.Context(native.Graph.from_alist(path), 0, 64)
+    f32 = prec == "f32"
+    v = VARIANTS[vname]
+    y = _glibc_frames(H.N, 8, 2.0, 0.5, seed=99)
+    if f32:
+        y = y.astype(np.float32)
+    A = O.Alist(path)
+    for T in (1, 2, 5, 12):
+        cfg = native.DecoderConfig(T=T, precision=native.F32 if f32 else native.F64, **v)
+        d, fr, cnt = ctx.decode(y, cfg)
+        want = A.decode(y, T, O.Cfg(**v))
+        assert int((d != want).sum()) == 0, T
+
+
+@pytest.mark.parametrize("vname", ["ms", "nms", "oms"])
+def test_signed_zeros_and_ties_exact(vname):
+    """Channel values drawn from {+-0, +-0.5, +-1, +-2}: exact zero messages
+    (sgn(-0) = +1, :518-523), tied minima (:428-437) and -0 channel samples. The
+    fast fp32 check node reads v2c signs from bit patterns, which holds only
+    because yq is canonicalised to +0; decisions must equal the oracle's."""
+    native = _native()
+    path = code_path("PEGReg504x1008.alist")
+    ctx = native.Context(native.Graph.from_alist(path), 0, 64)
+    A = O.Alist(path)
+    rng = np.random.default_rng(7)
+    vals = np.array([-0.0, 0.0, -0.5, 0.5, -1.0, 1.0, -2.0, 2.0], dtype=np.float32)
+    y = vals[rng.integers(0, len(vals), size=(16, A.N))]
+    y[:4] = np.where(rng.random((4, A.N)) < 0.5, np.float32(-0.0), np.float32(0.0))   # all-zero frames
+    v = VARIANTS[vname]
+    for T in (1, 2, 3, 8):
+        cfg = native.DecoderConfig(T=T, precision=native.F32, **v)
+        d, fr, cnt = ctx.decode(y, cfg)
+        want = A.decode(y, T, O.Cfg(**v))
+        assert int((d != want).sum()) == 0, T
