@@ -442,23 +442,34 @@ __device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DC], Pack<fl
                                         float alpha, float rcp)
 {
     constexpr uint32_t SIGN = 0x80000000u;
-    Pack<float, C> x[DC];
+    using V = float __attribute__((ext_vector_type(C)));   // C = 2: one v_pk_add_f32 per edge
+    V x[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k)
-#pragma unroll
-        for (int c = 0; c < C; ++c) x[k].v[c] = xin[k].v[c] - pv[k].v[c];          // v2c (:469)
+    for (int k = 0; k < DC; ++k) {
+        V xi, pi;
+        __builtin_memcpy(&xi, &xin[k], sizeof(V));
+        __builtin_memcpy(&pi, &pv[k], sizeof(V));
+        x[k] = xi - pi;                                                         // v2c (:469)
+    }
     bool ok = true;
+    // min(a, b) as med3(a, b, -inf) on an opaque -inf: the compiler would turn a
+    // visible -inf into v_min plus an input canonicalisation
+    float ninf = -__builtin_huge_valf();
+    asm("" : "+s"(ninf));
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         float mn1 = __builtin_huge_valf(), mn2 = __builtin_huge_valf();
         uint32_t par = 0;
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
-            const float ax = __builtin_fabsf(x[k].v[c]);
+            const float ax = __builtin_fabsf(x[k][c]);
             mn2 = __builtin_amdgcn_fmed3f(mn1, ax, mn2);
-            mn1 = __builtin_fminf(mn1, ax);
-            par ^= __float_as_uint(x[k].v[c]);
+            mn1 = __builtin_amdgcn_fmed3f(mn1, ax, ninf);
         }
+#pragma unroll
+        for (int k = 0; k + 1 < DC; k += 2)                                   // xor3
+            par = __builtin_amdgcn_bitop3_b32(par, __float_as_uint(x[k][c]), __float_as_uint(x[k + 1][c]), 0x96);
+        if (DC & 1) par ^= __float_as_uint(x[DC - 1][c]);
         float M1 = mn1, M2 = mn2;
         if (nms) {   // x/alpha = q + (x - q*alpha)*r, q = x*r (verified for all finite x); inf/alpha = inf
             const float q1 = mn1 * rcp, q2 = mn2 * rcp;
@@ -468,16 +479,17 @@ __device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DC], Pack<fl
             M2 = mn2 < __builtin_huge_valf() ? d2 : mn2;
         }
         ok &= M2 < 1e30f;
-        const uint32_t s1 = __float_as_uint(M1) ^ (par & SIGN), s2 = __float_as_uint(M2) ^ (par & SIGN);
+        uint32_t s1 = __float_as_uint(M1) ^ (par & SIGN), s2 = __float_as_uint(M2) ^ (par & SIGN);
+        asm("" : "+v"(s1), "+v"(s2));   // keep the parity out of the per-edge select
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
-            const uint32_t m = (__builtin_fabsf(x[k].v[c]) == mn1) ? s2 : s1;
-            pv[k].v[c] = __uint_as_float(m ^ (__float_as_uint(x[k].v[c]) & SIGN));
+            const uint32_t m = (__builtin_fabsf(x[k][c]) == mn1) ? s2 : s1;
+            // m ^ (v2c_k & SIGN)
+            pv[k].v[c] = __uint_as_float(__builtin_amdgcn_bitop3_b32(m, __float_as_uint(x[k][c]), SIGN, 0x78));
         }
     }
     return ok;
 }
-
 template <int DC, int C>
 __device__ __forceinline__ bool cn_fast(const Pack<double, C> (&)[DC], Pack<double, C> (&)[DC], bool, float, float)
 {
