@@ -164,6 +164,11 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
             }
         }
     }
+    // the kernel's bit-node phases rely on non-increasing group degree along a thread's slots
+    for (int t = 0; t < threads; ++t)
+        for (int i = 1; i < cpt; ++i)
+            if ((s.vn_info[(size_t)t * cpt + i] >> 24) > (s.vn_info[(size_t)t * cpt + i - 1] >> 24))
+                return "internal: bit slots not in non-increasing degree";
     return "";
 }
 

@@ -356,19 +356,58 @@ __device__ __forceinline__ float nms_div<float>(float x, float alpha, const Deco
     return x / alpha;
 }
 
-// sum += c2v[base + k*64] for k in [k0, min(k0+K, gd)), loads issued first.
-template <typename F, int C, int K>
-__device__ __forceinline__ void vn_accumulate(const Pack<F, C> *c2v, int base, int gd, int k0, F (&sum)[C])
+// s += r for every codeword of a pack (one v_pk_add_f32 for two fp32 codewords).
+template <typename F, int C>
+__device__ __forceinline__ void padd(Pack<F, C> &s, const Pack<F, C> &r)
 {
-    Pack<F, C> r[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) r[j] = c2v[base + (k0 + j < gd ? k0 + j : k0) * 64];
+    for (int c = 0; c < C; ++c) s.v[c] += r.v[c];
+}
+template <>
+__device__ __forceinline__ void padd<float, 2>(Pack<float, 2> &s, const Pack<float, 2> &r)
+{
+    using V = float __attribute__((ext_vector_type(2)));
+    V a, b;
+    __builtin_memcpy(&a, &s, sizeof(V));
+    __builtin_memcpy(&b, &r, sizeof(V));
+    a += b;
+    __builtin_memcpy(&s, &a, sizeof(V));
+}
+
+// Bit nodes, edges k in [k, kend) of the first NACT slots (every one of them has
+// group degree >= kend): sum_i += c2v[base_i + k*64] (c2v already offset by the
+// lane, base_i wave-uniform), in edge order per slot,
+// U edges of every slot in flight per step.
+template <typename F, int C, int NACT, int CPT>
+__device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base)[CPT], int &k, int kend,
+                                         Pack<F, C> (&sum)[CPT])
+{
+    constexpr int U = NACT >= 3 ? 2 : 4;   // at most 8 packs in flight
+    for (; k + U <= kend; k += U) {
+        Pack<F, C> r[NACT][U];
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-        if (k0 + j < gd) {
+        for (int i = 0; i < NACT; ++i)
 #pragma unroll
-            for (int c = 0; c < C; ++c) sum[c] += r[j].v[c];
-        }
+            for (int u = 0; u < U; ++u) r[i][u] = c2v[base[i] + (k + u) * 64];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int i = 0; i < NACT; ++i) padd(sum[i], r[i][u]);
+    }
+    for (; k < kend; ++k) {
+        Pack<F, C> r[NACT];
+#pragma unroll
+        for (int i = 0; i < NACT; ++i) r[i] = c2v[base[i] + k * 64];
+#pragma unroll
+        for (int i = 0; i < NACT; ++i) padd(sum[i], r[i]);
+    }
+}
+template <typename F, int C, int NACT, int CPT>
+__device__ __forceinline__ void vn_phases(const Pack<F, C> *c2v, const int (&base)[CPT], const int (&gd)[CPT], int &k,
+                                          Pack<F, C> (&sum)[CPT])
+{
+    vn_phase<F, C, NACT, CPT>(c2v, base, k, gd[NACT - 1], sum);
+    if constexpr (NACT > 1) vn_phases<F, C, NACT - 1, CPT>(c2v, base, gd, k, sum);
 }
 
 // Check node, exact path: the reference's comparisons for any input, incl.
@@ -481,9 +520,14 @@ __device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DC], Pack<fl
         ok &= M2 < 1e30f;
         uint32_t s1 = __float_as_uint(M1) ^ (par & SIGN), s2 = __float_as_uint(M2) ^ (par & SIGN);
         asm("" : "+v"(s1), "+v"(s2));   // keep the parity out of the per-edge select
+        // all compares first (separate lane masks), then the selects: no
+        // compare->select hazard wait states between neighbours
+        bool eq[DC];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) eq[k] = __builtin_fabsf(x[k][c]) == mn1;
 #pragma unroll
         for (int k = 0; k < DC; ++k) {
-            const uint32_t m = (__builtin_fabsf(x[k][c]) == mn1) ? s2 : s1;
+            const uint32_t m = eq[k] ? s2 : s1;
             // m ^ (v2c_k & SIGN)
             pv[k].v[c] = __uint_as_float(__builtin_amdgcn_bitop3_b32(m, __float_as_uint(x[k][c]), SIGN, 0x78));
         }
@@ -537,14 +581,22 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
             posw[r][4 * q + 0] = xp.x; posw[r][4 * q + 1] = xp.y; posw[r][4 * q + 2] = xp.z; posw[r][4 * q + 3] = xp.w;
         }
     }
-    int vcol[CPT];
-    uint32_t vinfo[CPT];
+    // bit slots: a thread's slots have non-increasing group degree (graph.cpp)
+    // Slot i of lane l: c2v edge k at vgb[i] + l + 64k (vgb and the group degree
+    // vgd are wave-uniform: SGPRs); the bit it sums into is vdst (two 16-bit
+    // entries per register; the spare app entry N+1 for an empty slot).
+    const int lane = tid & 63;
+    int vgb[CPT], vgd[CPT];
+    uint32_t vdst2[(CPT + 1) / 2] = {};
 #pragma unroll
     for (int i = 0; i < CPT; ++i) {
         const int c = rs.vn_col[tid * CPT + i];
-        vcol[i] = c == 0xffff ? -1 : c;
-        vinfo[i] = rs.vn_info[tid * CPT + i];
+        vdst2[i / 2] |= (uint32_t)(c == 0xffff ? N + 1 : c) << (16 * (i & 1));
+        const uint32_t info = rs.vn_info[tid * CPT + i];
+        vgb[i] = __builtin_amdgcn_readfirstlane((int)(info & 0xffffu) - lane);
+        vgd[i] = __builtin_amdgcn_readfirstlane((int)(info >> 24));
     }
+    auto vdst = [&](int i) -> int { return (int)((vdst2[i / 2] >> (16 * (i & 1))) & 0xffffu); };
     if (tid == 0) {
         P inf;
 #pragma unroll
@@ -603,18 +655,16 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
             }
         }
         __syncthreads();
-        F yq[C][CPT];
+        P yq[CPT];
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
-            const int v = vcol[i];
-            const P st = c2v[v >= 0 ? v : 0];
+            const P st = c2v[vdst(i) <= N ? vdst(i) : 0];
             // yq + 0 maps -0 to +0, so app is never -0: v2c = app - c2v differs
             // at most in the sign of a zero, which sgn() and |.| ignore, and
             // the decision app > 0 is the same (the fast check node relies on it)
-            P q;
 #pragma unroll
-            for (int c = 0; c < C; ++c) q.v[c] = yq[c][i] = st.v[c] + F(0);
-            if (v >= 0) app[v] = q;   // v2c = yq on the first pass (:364-370)
+            for (int c = 0; c < C; ++c) yq[i].v[c] = st.v[c] + F(0);
+            app[vdst(i)] = yq[i];   // v2c = yq on the first pass (:364-370)
         }
         if (tid == 0) red[31] = 0;     // fast check-node path allowed
         __syncthreads();
@@ -622,8 +672,8 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
         // sum, and hence every decision, unchanged).
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
-            const int base = (int)(vinfo[i] & 0xffffu), dg = (int)((vinfo[i] >> 16) & 0xffu);
-            const int gd = (int)(vinfo[i] >> 24);
+            const int dg = (int)((rs.vn_info[tid * CPT + i] >> 16) & 0xffu);
+            const int base = vgb[i] + lane, gd = vgd[i];
             P z;
 #pragma unroll
             for (int c = 0; c < C; ++c) z.v[c] = F(0);
@@ -700,29 +750,16 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
 #ifdef LDPC_STAMPS
                 st_cn += t_vn0 - t_cn0;
 #endif
-                // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
+                // ---- bit nodes: sum = yq + c2v in nlist order (:452-476); edges past a
+                // bit's own degree hold +0 ----
+                {
+                    P sum[CPT];
 #pragma unroll
-                for (int i = 0; i < CPT; ++i) {
-                    const int gd = __builtin_amdgcn_readfirstlane((int)(vinfo[i] >> 24));   // wave-uniform
-                    if (gd == 0) continue;
-                    const int v = vcol[i];
-                    const int base = (int)(vinfo[i] & 0xffffu);
-                    F sum[C];
+                    for (int i = 0; i < CPT; ++i) sum[i] = yq[i];
+                    int k = 0;
+                    vn_phases<F, C, CPT, CPT>(c2v + lane, vgb, vgd, k, sum);
 #pragma unroll
-                    for (int c = 0; c < C; ++c) sum[c] = yq[c][i];
-                    // all of a slot's reads in flight before the first add; edges past a
-                    // bit's own degree hold +0
-                    if (gd <= 4) vn_accumulate<F, C, 4>(c2v, base, gd, 0, sum);
-                    else if (gd <= 8) vn_accumulate<F, C, 8>(c2v, base, gd, 0, sum);
-                    else if (gd <= 12) vn_accumulate<F, C, 12>(c2v, base, gd, 0, sum);
-                    else
-                        for (int k0 = 0; k0 < gd; k0 += 8) vn_accumulate<F, C, 8>(c2v, base, gd, k0, sum);
-                    if (v >= 0) {
-                        P o;
-#pragma unroll
-                        for (int c = 0; c < C; ++c) o.v[c] = sum[c];
-                        app[v] = o;
-                    }
+                    for (int i = 0; i < CPT; ++i) app[vdst(i)] = sum[i];
                 }
                 __syncthreads();
 #ifdef LDPC_STAMPS
@@ -746,8 +783,8 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
             if (valid) {
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) {
-                    const int v = vcol[i];
-                    if (v >= 0) {
+                    const int v = vdst(i);
+                    if (v < N) {
                         const int d = app[v].v[c] > F(0) ? 1 : -1;
                         const int cv = cvec[c] ? cvec[c][v] : 1;
                         w += (d != cv);
