@@ -23,6 +23,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 
 namespace ldpc {
@@ -129,6 +130,28 @@ __device__ __forceinline__ int block_sum(int x, int *red)
     const int nw = (blockDim.x + 63) >> 6;
     for (int i = 0; i < nw; ++i) s += red[i];
     return s;
+}
+
+// Sums of NV values over the workgroup with one barrier pair; red holds 16*NV ints.
+template <int NV>
+__device__ __forceinline__ void block_sum_n(int (&x)[NV], int *red)
+{
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x[v] += __shfl_xor(x[v], o, 64);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = (blockDim.x + 63) >> 6;
+    __syncthreads();
+    if (l == 0)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) red[w * NV + v] = x[v];
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        int t = 0;
+        for (int i = 0; i < nw; ++i) t += red[i * NV + v];
+        x[v] = t;
+    }
 }
 
 // ---------------------------------------------------------------------
@@ -376,8 +399,9 @@ __device__ __forceinline__ void padd<float, 2>(Pack<float, 2> &s, const Pack<flo
 
 // Bit nodes, edges k in [k, kend) of the first NACT slots (every one of them has
 // group degree >= kend): sum_i += c2v[base_i + k*64] (c2v already offset by the
-// lane, base_i wave-uniform), in edge order per slot,
-// U edges of every slot in flight per step.
+// lane, base_i wave-uniform), in edge order per slot, U edges of every slot in
+// flight per step. (Steps sized exactly to the remainder were measured slower:
+// the extra unrolled variants cost more in instruction fetch than they save.)
 template <typename F, int C, int NACT, int CPT>
 __device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base)[CPT], int &k, int kend,
                                          Pack<F, C> (&sum)[CPT])
@@ -491,20 +515,45 @@ __device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DC], Pack<fl
         x[k] = xi - pi;                                                         // v2c (:469)
     }
     bool ok = true;
-    // min(a, b) as med3(a, b, -inf) on an opaque -inf: the compiler would turn a
-    // visible -inf into v_min plus an input canonicalisation
-    float ninf = -__builtin_huge_valf();
-    asm("" : "+s"(ninf));
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        float mn1 = __builtin_huge_valf(), mn2 = __builtin_huge_valf();
-        uint32_t par = 0;
+        // (m1, m2) = the two smallest |v2c| of the row, by groups of three
+        // (lo, sec) = (min3, med3), merged with sec' = med3(lo, lo_g, min(sec, sec_g))
+        // (or, for three groups, min(med3(lo_1..3), min3(sec_1..3))).
+        constexpr int G = (DC + 2) / 3;
+        float lo[G], sec[G];
 #pragma unroll
-        for (int k = 0; k < DC; ++k) {
-            const float ax = __builtin_fabsf(x[k][c]);
-            mn2 = __builtin_amdgcn_fmed3f(mn1, ax, mn2);
-            mn1 = __builtin_amdgcn_fmed3f(mn1, ax, ninf);
+        for (int g = 0; g < G; ++g) {
+            const int k0 = 3 * g, n = DC - k0 < 3 ? DC - k0 : 3;
+            const float a0 = __builtin_fabsf(x[k0][c]);
+            if (n == 3) {
+                const float a1 = __builtin_fabsf(x[k0 + 1][c]), a2 = __builtin_fabsf(x[k0 + 2][c]);
+                lo[g] = __builtin_fminf(__builtin_fminf(a0, a1), a2);
+                sec[g] = __builtin_amdgcn_fmed3f(a0, a1, a2);
+            } else if (n == 2) {
+                const float a1 = __builtin_fabsf(x[k0 + 1][c]);
+                lo[g] = __builtin_fminf(a0, a1);
+                sec[g] = __builtin_fmaxf(a0, a1);
+            } else {
+                lo[g] = a0;
+                sec[g] = __builtin_huge_valf();
+            }
         }
+        float mn1, mn2;
+        if constexpr (G == 3) {
+            mn1 = __builtin_fminf(__builtin_fminf(lo[0], lo[1]), lo[2]);
+            mn2 = __builtin_fminf(__builtin_amdgcn_fmed3f(lo[0], lo[1], lo[2]),
+                                  __builtin_fminf(__builtin_fminf(sec[0], sec[1]), sec[2]));
+        } else {
+            mn1 = lo[0];
+            mn2 = sec[0];
+#pragma unroll
+            for (int g = 1; g < G; ++g) {
+                mn2 = __builtin_amdgcn_fmed3f(mn1, lo[g], __builtin_fminf(mn2, sec[g]));
+                mn1 = __builtin_fminf(mn1, lo[g]);
+            }
+        }
+        uint32_t par = 0;
 #pragma unroll
         for (int k = 0; k + 1 < DC; k += 2)                                   // xor3
             par = __builtin_amdgcn_bitop3_b32(par, __float_as_uint(x[k][c]), __float_as_uint(x[k + 1][c]), 0x96);
@@ -608,6 +657,8 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
     const int ngrp = (a.batch + C - 1) / C;
     unsigned long long st_chan = 0, st_cn = 0, st_vn = 0, st_acct = 0;
     (void)st_chan; (void)st_cn; (void)st_vn; (void)st_acct;
+    // the block's totals (thread 0), added to a.counts once at the end
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
     for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
         STAMP(t_start);
         // ---- channel (:214-238), staged through the c2v area ----
@@ -716,27 +767,36 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
         auto iterate = [&](auto fast_tag, int it0) -> int {
             constexpr bool FAST = decltype(fast_tag)::value;
             int it = it0;
+            // fast-path flag: read right after the check-node barrier of the previous
+            // iteration (in flight during the bit-node phase), so no LDS round trip
+            // opens the iteration; red[31] was cleared before the first iteration
+            int flag = 0;
             for (; it < a.T; ++it) {
                 STAMP(t_cn0);
-                if (FAST && __builtin_amdgcn_readfirstlane(red[31]) != 0) break;
-                // ---- check nodes (:410-450, :494-515) ----
+                if (FAST && __builtin_amdgcn_readfirstlane(flag) != 0) break;
+                // ---- check nodes (:410-450, :494-515); row r+1's gathers are issued
+                // before row r is computed ----
+                P xin[2][DC];
+#pragma unroll
+                for (int k = 0; k < DC; ++k) xin[0][k] = app[u16_at<DC>(colw[0], k)];   // padding edges read +INF
 #pragma unroll
                 for (int r = 0; r < RPT; ++r) {
-                    P xin[DC];
+                    if (r + 1 < RPT) {
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) xin[k] = app[u16_at<DC>(colw[r], k)];   // padding edges read +INF
+                        for (int k = 0; k < DC; ++k) xin[(r + 1) & 1][k] = app[u16_at<DC>(colw[r + 1 < RPT ? r + 1 : r], k)];
+                    }
                     P (&pv)[DC] = prev[PREV_REG ? r : 0];
                     if (!PREV_REG) {
 #pragma unroll
                         for (int k = 0; k < DC; ++k) pv[k] = c2v[u16_at<DC>(posw[r], k)];
                     }
                     if constexpr (FAST) {
-                        const bool ok = cn_fast<DC, C>(xin, pv, a.variant == V_NMS, (float)alpha, a.alpha_rcp);
+                        const bool ok = cn_fast<DC, C>(xin[r & 1], pv, a.variant == V_NMS, (float)alpha, a.alpha_rcp);
                         // Rows past M (degree 0) only write the never-read dummy slots.
                         if (!ok && deg[r] > 0) red[31] = 1;
                     } else {
 #pragma unroll
-                        for (int c = 0; c < C; ++c) cn_exact<F, C, DC>(xin, c, pv, degmask[r], a, alpha, delta);
+                        for (int c = 0; c < C; ++c) cn_exact<F, C, DC>(xin[r & 1], c, pv, degmask[r], a, alpha, delta);
                     }
 #pragma unroll
                     for (int k = 0; k < DC; ++k) c2v[u16_at<DC>(posw[r], k)] = pv[k];   // padding edges: the lane's dummy slot
@@ -746,6 +806,7 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
 #endif
                 }
                 __syncthreads();
+                if (FAST) flag = red[31];
                 STAMP(t_vn0);
 #ifdef LDPC_STAMPS
                 st_cn += t_vn0 - t_cn0;
@@ -775,12 +836,12 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
         STAMP(t_acct0);
 
         // ---- decisions, error weight, syndrome, accounting ----
+        int sums[3 * C];   // per codeword: error weight, uncoded errors, syndrome failure
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             const int b = grp * C + c;
-            const bool valid = b < a.batch;
             int w = 0, synd = 0;
-            if (valid) {
+            if (b < a.batch) {
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) {
                     const int v = vdst(i);
@@ -791,33 +852,44 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
                         if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
                     }
                 }
+                // padding edges read the +inf sentinel: parity 0
 #pragma unroll
                 for (int r = 0; r < RPT; ++r) {
                     int par = 0;
 #pragma unroll
-                    for (int k = 0; k < DC; ++k)
-                        if (k < deg[r]) par ^= (app[u16_at<DC>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
+                    for (int k = 0; k < DC; ++k) par ^= (app[u16_at<DC>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
                     synd |= par;
                 }
             }
-            w = block_sum(w, red);
-            const int uc = block_sum(unc[c], red);
-            synd = block_sum(synd, red);
-            if (tid == 0 && valid) {
-                atomicAdd(&a.counts[0], (unsigned long long)w);
-                atomicAdd(&a.counts[1], (unsigned long long)(w > 0));
-                atomicAdd(&a.counts[2], (unsigned long long)uc);
-                atomicAdd(&a.counts[3], 1ull);
-                atomicAdd(&a.counts[4], (unsigned long long)a.T);
-                atomicAdd(&a.counts[5], (unsigned long long)(synd > 0));
+            sums[3 * c] = w;
+            sums[3 * c + 1] = unc[c];
+            sums[3 * c + 2] = synd;
+        }
+        block_sum_n<3 * C>(sums, red + 32);
+        if (tid == 0) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int b = grp * C + c;
+                if (b >= a.batch) continue;
+                const int w = sums[3 * c], uc = sums[3 * c + 1], sf = sums[3 * c + 2] > 0;
+                acc[0] += (unsigned long long)w;
+                acc[1] += (unsigned long long)(w > 0);
+                acc[2] += (unsigned long long)uc;
+                acc[3] += 1ull;
+                acc[5] += (unsigned long long)sf;
                 if (w > 0 && a.hist) atomicAdd(&a.hist[w - 1], 1ull);
-                if (a.frame_res) a.frame_res[b] = make_int4(w, uc, synd > 0 ? 1 : 0, 0);
+                if (a.frame_res) a.frame_res[b] = make_int4(w, uc, sf, 0);
             }
         }
         __syncthreads();
 #ifdef LDPC_STAMPS
         { STAMP(t_end); st_acct += t_end - t_acct0; }
 #endif
+    }
+    if (tid == 0 && acc[3] > 0) {
+        acc[4] = acc[3] * (unsigned long long)a.T;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) atomicAdd(&a.counts[q], acc[q]);
     }
 #ifdef LDPC_STAMPS
     if (tid == 0 && a.stamps) {
@@ -878,7 +950,8 @@ static int rows_cw_per_block(bool f64, int dc)
 static size_t rows_lds(const DevGraph &g, const RowSched &rs, bool f64, int C)
 {
     const size_t fs = f64 ? 8 : 4;
-    return ((size_t)C * ((size_t)g.N + 2 + (size_t)rs.e_pad + 64) * fs + 128 + 15) & ~(size_t)15;
+    // + red: 32 ints (fast-path flag at [31]) and 16 waves x 8 sums
+    return ((size_t)C * ((size_t)g.N + 2 + (size_t)rs.e_pad + 64) * fs + 4 * (32 + 16 * 8) + 15) & ~(size_t)15;
 }
 
 KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force)
@@ -943,6 +1016,8 @@ static hipError_t launch_rows_t(const DevGraph &g, const RowSched &rs, const Dec
     int per_cu = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kc.threads, kc.lds_bytes);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    if (const char *cap = std::getenv("LDPC_BLOCKS_PER_CU"))   // diagnostic: fewer resident blocks
+        if (std::atoi(cap) >= 1 && std::atoi(cap) < per_cu) per_cu = std::atoi(cap);
     const int ngrp = (a.batch + C - 1) / C;
     int grid = per_cu * num_cus;
     if (grid > ngrp) grid = ngrp;

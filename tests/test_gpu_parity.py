@@ -67,6 +67,8 @@ def test_decisions_bit_exact_vs_oracle(gpu_ctx_factory, code, vname, prec):
     if f32:
         y = y.astype(np.float32)
     A = O.Alist(code_path(code))
+    from ldpcsimulation_amd import codes
+    H = codes.read_alist(code_path(code))
     yq = _oracle_front(y, v, f32)
     for T in (0, 1, 3, 10):
         cfg = native.DecoderConfig(T=T, precision=native.F32 if f32 else native.F64, **v)
@@ -78,6 +80,8 @@ def test_decisions_bit_exact_vs_oracle(gpu_ctx_factory, code, vname, prec):
         assert np.array_equal(fr["bit_err"], w)
         assert cnt.frames == len(y) and cnt.bit_err == int(w.sum())
         assert cnt.frame_err == int((w > 0).sum()) and cnt.iters == T * len(y)
+        sf = [int(any(H.syndrome(row != 1))) for row in want]
+        assert list(fr["syndrome_fail"]) == sf and cnt.syndrome_fail == sum(sf)
 
 
 @pytest.mark.parametrize("run", golden_runs(), ids=lambda r: r["name"])
