@@ -22,8 +22,11 @@ $(LIBDIR)/obj:
 $(BINDIR):
 	mkdir -p $@
 
+# -load-store-opt: keep the bit-phase LDS reads as single ds_read_b64 (2 LDS
+# cycles each) instead of merged ds_read2st64_b64 (8 cycles for the same data).
+KERNFLAGS = -Xclang -target-feature -Xclang -load-store-opt
 $(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h | $(LIBDIR)/obj
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/api.o: $(CSRC)/api.cpp $(CSRC)/kernels.h $(CSRC)/graph.h include/ldpc_hip.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/graph.o: $(CSRC)/graph.cpp $(CSRC)/graph.h | $(LIBDIR)/obj
@@ -48,7 +51,7 @@ $(BINDIR)/decodeOffsetMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
 # Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> lib/variants/libldpc_hip_x.so
 variant:
 	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/api.o $(CSRC)/api.cpp
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/graph.o
