@@ -76,10 +76,13 @@ struct ldpc_ctx {
     int cw_rows = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
-    char force[16] = {0};        // LDPC_KERNEL=lds|global (LDPC_FORCE_GLOBAL=1 = global), tests only
+    char force[16] = {0};        // LDPC_KERNEL=lds|flood|global (LDPC_FORCE_GLOBAL=1 = global), tests only
     bool has_rs = false;
     ldpc::RowSched rs{};
     DevBuf sched;
+    bool has_fs = false;
+    ldpc::FloodSched fs{};
+    DevBuf fsched;                                        // flood kernel schedule (codes beyond LDS)
     DevBuf divcheck;                                      // mismatch counter of verify_div_by_reciprocal
     std::vector<std::pair<float, bool>> div_ok;           // alpha -> reciprocal division exact
 };
@@ -168,7 +171,7 @@ static void ctx_free(ldpc_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->graph, &c->counts, &c->hist, &c->y_stage, &c->c_stage, &c->d_stage, &c->fw_stage,
-                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck})
+                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck, &c->fsched})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -282,6 +285,39 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
             c->has_rs = true;
         }
     }
+    // Flood schedule (global-memory kernel for codes whose state exceeds LDS;
+    // also selectable with LDPC_KERNEL=flood for tests).
+    {
+        ldpc::FloodSchedule fh;
+        if (ldpc::build_flood_schedule(*g, fh).empty()) {
+            const size_t n_sp = fh.sp.size(), n_rd = fh.rdeg.size(), n_pb = fh.pos_of_bit.size(),
+                         n_ba = fh.bit_at.size(), n_pd = fh.pdeg.size(), n_gb = fh.gbase.size();
+            const size_t o_sq = al(4 * n_sp), o_rd = o_sq + al(4 * n_sp), o_pb = o_rd + al(n_rd),
+                         o_ba = o_pb + al(4 * n_pb), o_pd = o_ba + al(4 * n_ba), o_gb = o_pd + al(n_pd),
+                         tot = o_gb + al(4 * n_gb);
+            CTX_TRY(c->fsched.ensure(tot));
+            unsigned char *fb = (unsigned char *)c->fsched.p;
+            CTX_TRY(hipMemcpy(fb, fh.sp.data(), 4 * n_sp, hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(fb + o_sq, fh.sq.data(), 4 * n_sp, hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(fb + o_rd, fh.rdeg.data(), n_rd, hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(fb + o_pb, fh.pos_of_bit.data(), 4 * n_pb, hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(fb + o_ba, fh.bit_at.data(), 4 * n_ba, hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(fb + o_pd, fh.pdeg.data(), n_pd, hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(fb + o_gb, fh.gbase.data(), 4 * n_gb, hipMemcpyHostToDevice));
+            c->fs.M_pad = fh.M_pad;
+            c->fs.dc = fh.dc;
+            c->fs.ngroups = fh.ngroups;
+            c->fs.e_pad = fh.e_pad;
+            c->fs.sp = (const int32_t *)fb;
+            c->fs.sq = (const int32_t *)(fb + o_sq);
+            c->fs.rdeg = (const uint8_t *)(fb + o_rd);
+            c->fs.pos_of_bit = (const int32_t *)(fb + o_pb);
+            c->fs.bit_at = (const int32_t *)(fb + o_ba);
+            c->fs.pdeg = (const uint8_t *)(fb + o_pd);
+            c->fs.gbase = (const int32_t *)(fb + o_gb);
+            c->has_fs = true;
+        }
+    }
     CTX_TRY(c->counts.ensure(8 * sizeof(unsigned long long)));
     CTX_TRY(hipMemset(c->counts.p, 0, c->counts.n));
     CTX_TRY(c->hist.ensure(sizeof(unsigned long long) * (size_t)g->N));
@@ -385,7 +421,8 @@ static int nms_setup(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, ldpc::DecodeArgs 
 static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64)
 {
     const ldpc::KernelChoice kc =
-        ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr);
+        ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr,
+                            c->has_fs ? &c->fs : nullptr);
     int gblocks = 0;
     if (kc.scratch_per_block) {
         int per_cu = ldpc::blocks_per_cu(c->dg, f64, kc);
@@ -408,7 +445,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64)
 #endif
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream, c->has_rs ? &c->rs : nullptr,
-                                c->num_cus));
+                                c->num_cus, c->has_fs ? &c->fs : nullptr));
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
 #ifdef LDPC_STAMPS
@@ -694,7 +731,8 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     HIP_TRY(hipSetDevice(c->device));
     const bool f64 = cfg->precision == LDPC_F64;
     const ldpc::KernelChoice kc =
-        ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr);
+        ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr,
+                            c->has_fs ? &c->fs : nullptr);
     if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", kc.name);
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
     if (bpc) *bpc = ldpc::blocks_per_cu(c->dg, f64, kc);

@@ -203,3 +203,212 @@ std::string load_alist(const char *path, ldpc_graph &g)
 }
 
 }  // namespace ldpc
+
+namespace ldpc {
+
+// Chains from a successor vote: next[x] = the candidate with most votes (>= minv),
+// each node taking at most one predecessor; the result lists every node once,
+// chain by chain (cycles broken at their smallest unvisited node).
+static std::vector<int> chain_order(int n, const std::vector<int> &next)
+{
+    std::vector<int> pred(n, -1), nx(n, -1);
+    for (int x = 0; x < n; ++x)
+        if (next[x] >= 0 && pred[next[x]] < 0 && next[x] != x) {
+            nx[x] = next[x];
+            pred[next[x]] = x;
+        }
+    std::vector<char> seen(n, 0);
+    std::vector<int> order;
+    order.reserve(n);
+    auto walk = [&](int h) {
+        for (int x = h; x >= 0 && !seen[x]; x = nx[x]) {
+            seen[x] = 1;
+            order.push_back(x);
+        }
+    };
+    for (int x = 0; x < n; ++x)
+        if (pred[x] < 0) walk(x);   // chain heads
+    for (int x = 0; x < n; ++x)
+        if (!seen[x]) walk(x);      // pure cycles
+    return order;
+}
+
+std::string build_flood_schedule(const ldpc_graph &g, FloodSchedule &s)
+{
+    s = FloodSchedule();
+    const int N = g.N, M = g.M, dcs = std::max(g.maxdc, 1);
+    if (g.maxdc > 26) return "row degree exceeds the flood kernel's packed row state";
+    s.dc = std::max(g.maxdc, 1);
+    // rows of each bit
+    auto rows_of = [&](int c, int e) { return (int)(g.col_refs[g.col_ptr[c] + e] >> kRefShift); };
+    // ---- row chains: successor = the row holding most of (columns + 1) ----
+    std::vector<int> rnext(M, -1);
+    {
+        std::vector<int> cnt(M, 0), touched;
+        for (int j = 0; j < M; ++j) {
+            touched.clear();
+            const int d = g.row_deg[j];
+            for (int k = 0; k < d; ++k) {
+                const int c = g.row_cols[(size_t)j * dcs + k] + 1;
+                if (c >= N) continue;
+                for (int e = 0; e < g.col_deg[c]; ++e) {
+                    const int j2 = rows_of(c, e);
+                    if (cnt[j2]++ == 0) touched.push_back(j2);
+                }
+            }
+            int best = -1;
+            for (int j2 : touched) {
+                if (j2 != j && cnt[j2] >= 2 && 2 * cnt[j2] >= d && (best < 0 || cnt[j2] > cnt[best])) best = j2;
+            }
+            for (int j2 : touched) cnt[j2] = 0;
+            rnext[j] = best;
+        }
+    }
+    const std::vector<int> rorder = chain_order(M, rnext);
+    // ---- slot alignment along the chains: slot k of the next row holds the
+    // column matching slot k of this row (c + 1 first, the rest in sorted order) ----
+    std::vector<std::vector<int>> slots(M);   // per row: original edge index k of each slot
+    std::vector<int> rpos(M);
+    for (int i = 0; i < M; ++i) rpos[rorder[i]] = i;
+    std::vector<char> placed(M, 0);
+    for (int i = 0; i < M; ++i) {
+        const int j = rorder[i];
+        const int d = g.row_deg[j];
+        const int *rc = &g.row_cols[(size_t)j * dcs];
+        const int jp = (i > 0 && rnext[rorder[i - 1]] == j) ? rorder[i - 1] : -1;   // chain predecessor
+        if (jp < 0 || !placed[jp]) {   // chain head: slots by column index
+            std::vector<int> ks(d);
+            for (int k = 0; k < d; ++k) ks[k] = k;
+            std::sort(ks.begin(), ks.end(), [&](int a, int b) { return rc[a] < rc[b]; });
+            slots[j] = ks;
+        } else {
+            const int *pc = &g.row_cols[(size_t)jp * dcs];
+            const std::vector<int> &ps = slots[jp];
+            std::vector<int> ks(d, -1);
+            std::vector<char> used(d, 0);
+            for (size_t t = 0; t < ps.size() && t < (size_t)d; ++t) {   // c + 1 matches
+                const int want = pc[ps[t]] + 1;
+                for (int k = 0; k < d; ++k)
+                    if (!used[k] && rc[k] == want) { ks[t] = k; used[k] = 1; break; }
+            }
+            std::vector<int> restk;
+            for (int k = 0; k < d; ++k)
+                if (!used[k]) restk.push_back(k);
+            std::sort(restk.begin(), restk.end(), [&](int a, int b) { return rc[a] < rc[b]; });
+            size_t r = 0;
+            for (int t = 0; t < d; ++t)
+                if (ks[t] < 0) ks[t] = restk[r++];
+            slots[j] = ks;
+        }
+        placed[j] = 1;
+    }
+    // ---- bit chains: c -> the column in the same slot of the next row ----
+    std::vector<int> cnext(N, -1);
+    {
+        std::vector<std::vector<std::pair<int, int>>> votes(N);
+        for (int i = 0; i + 1 < M; ++i) {
+            const int j = rorder[i], j2 = rorder[i + 1];
+            if (rnext[j] != j2) continue;
+            const int d = std::min<int>(g.row_deg[j], g.row_deg[j2]);
+            for (int t = 0; t < d; ++t) {
+                const int c = g.row_cols[(size_t)j * dcs + slots[j][t]];
+                const int c2 = g.row_cols[(size_t)j2 * dcs + slots[j2][t]];
+                auto &v = votes[c];
+                bool hit = false;
+                for (auto &pr : v)
+                    if (pr.first == c2) { ++pr.second; hit = true; break; }
+                if (!hit) v.push_back({c2, 1});
+            }
+        }
+        for (int c = 0; c < N; ++c) {
+            int best = -1, bv = 0;
+            for (auto &pr : votes[c])
+                if (pr.second > bv) { bv = pr.second; best = pr.first; }
+            cnext[c] = best;
+        }
+    }
+    // storage order: column chains in order of first use by (row order, slot)
+    std::vector<int> corder0 = chain_order(N, cnext);
+    std::vector<int> chain_id(N, -1), chain_start;
+    {
+        // split corder0 into chains (a chain continues while cnext links consecutive entries)
+        for (int t = 0; t < N; ++t) {
+            if (t == 0 || cnext[corder0[t - 1]] != corder0[t]) chain_start.push_back(t);
+            chain_id[corder0[t]] = (int)chain_start.size() - 1;
+        }
+    }
+    chain_start.push_back(N);
+    std::vector<int> corder;
+    corder.reserve(N);
+    {
+        std::vector<char> done(chain_start.size(), 0);
+        auto emit = [&](int ch) {
+            if (done[ch]) return;
+            done[ch] = 1;
+            for (int t = chain_start[ch]; t < chain_start[ch + 1]; ++t) corder.push_back(corder0[t]);
+        };
+        for (int i = 0; i < M; ++i) {
+            const int j = rorder[i];
+            for (int t = 0; t < (int)slots[j].size(); ++t)
+                emit(chain_id[g.row_cols[(size_t)j * dcs + slots[j][t]]]);
+        }
+        for (int ch = 0; ch + 1 < (int)chain_start.size(); ++ch) emit(ch);
+    }
+    // ---- layouts ----
+    s.ngroups = (N + 63) / 64;
+    const int NP = s.ngroups * 64;
+    s.pos_of_bit.assign(N, -1);
+    s.bit_at.assign(NP, -1);
+    s.pdeg.assign(NP, 0);
+    for (int p = 0; p < N; ++p) {
+        s.pos_of_bit[corder[p]] = p;
+        s.bit_at[p] = corder[p];
+        s.pdeg[p] = g.col_deg[corder[p]];
+    }
+    s.gbase.assign(s.ngroups, 0);
+    long base = 0;
+    for (int gi = 0; gi < s.ngroups; ++gi) {
+        int gd = 0;
+        for (int l = 0; l < 64; ++l) gd = std::max(gd, (int)s.pdeg[gi * 64 + l]);
+        s.gbase[gi] = (int32_t)base;
+        base += 64L * gd;
+    }
+    if (base + 64 > INT32_MAX) return "graph too large for the flood schedule";
+    s.e_pad = (int)base;
+    // c2v element of each edge (row j, original position k)
+    std::vector<int32_t> qpos((size_t)M * dcs, -1);
+    for (int c = 0; c < N; ++c) {
+        const int p = s.pos_of_bit[c];
+        for (int e = 0; e < g.col_deg[c]; ++e) {
+            const uint32_t ref = g.col_refs[g.col_ptr[c] + e];
+            const int j = (int)(ref >> kRefShift), k = (int)(ref & ((1u << kRefShift) - 1));
+            qpos[(size_t)j * dcs + k] = s.gbase[p / 64] + 64 * e + (p % 64);
+        }
+    }
+    s.M_pad = (M + 63) / 64 * 64;
+    s.row_of.assign(s.M_pad, -1);
+    s.rdeg.assign(s.M_pad, 0);
+    s.sp.assign((size_t)s.dc * s.M_pad, NP);   // padding slots: the +inf sentinel position NP
+    s.sq.assign((size_t)s.dc * s.M_pad, 0);
+    long coal = 0, tot = 0;
+    for (int i = 0; i < s.M_pad; ++i) {
+        for (int t = 0; t < s.dc; ++t) s.sq[(size_t)t * s.M_pad + i] = s.e_pad + (i & 63);
+        if (i >= M) continue;
+        const int j = rorder[i];
+        s.row_of[i] = j;
+        s.rdeg[i] = g.row_deg[j];
+        for (int t = 0; t < g.row_deg[j]; ++t) {
+            const int k = slots[j][t];
+            s.sp[(size_t)t * s.M_pad + i] = s.pos_of_bit[g.row_cols[(size_t)j * dcs + k]];
+            s.sq[(size_t)t * s.M_pad + i] = qpos[(size_t)j * dcs + k];
+            if (i & 63) {
+                ++tot;
+                coal += s.sp[(size_t)t * s.M_pad + i] == s.sp[(size_t)t * s.M_pad + i - 1] + 1;
+            }
+        }
+    }
+    s.coalesced = tot ? (double)coal / (double)tot : 0.0;
+    return "";
+}
+
+}  // namespace ldpc

@@ -47,6 +47,33 @@ struct RowSchedule {
 // an error message.
 std::string build_graph(int N, int M, const int *num_nlist, const int *const *nlist,
                         const int *num_mlist, const int *const *mlist, ldpc_graph &g);
+// Static schedule of the global-memory flooding kernel (kernels.hip,
+// k_decode_flood) for codes whose state does not fit on chip (DVB-S2 N=64800).
+// Quasi-cyclic structure is discovered, not assumed: every row is chained to
+// the row that holds most of its columns + 1, edge slots are aligned along the
+// chains, and columns are chained the same way (column c -> the column the
+// aligned slot of the next row holds). Rows are processed in chain order and
+// bits are stored in column-chain order, so the 64 lanes of a wave, working on
+// 64 consecutive rows of a chain, gather and scatter 64 consecutive words
+// (DVB-S2: 90 row chains and the bit chains of length 360; 802.11n: Z=81).
+// Nothing depends on the discovery succeeding: a code without the structure
+// gets an arbitrary but valid order.
+struct FloodSchedule {
+    int M_pad = 0;                    // rows rounded up to 64
+    int dc = 0;                       // max row degree
+    int ngroups = 0, e_pad = 0;       // 64-bit groups of the c2v layout, its size
+    std::vector<int32_t> row_of;      // [M_pad] check row at order position i (-1: padding)
+    std::vector<uint8_t> rdeg;        // [M_pad]
+    std::vector<int32_t> sp;          // [dc * M_pad] slot-major: bit position (storage order) of slot k (pads: ngroups*64, the +inf sentinel)
+    std::vector<int32_t> sq;          // [dc * M_pad] slot-major: c2v element of slot k (pads: e_pad + i%64)
+    std::vector<int32_t> pos_of_bit;  // [N] storage position of bit v
+    std::vector<int32_t> bit_at;      // [ngroups * 64] bit at storage position p (-1: padding)
+    std::vector<uint8_t> pdeg;        // [ngroups * 64] degree of the bit at position p
+    std::vector<int32_t> gbase;       // [ngroups]: edge e (nlist order) of position p at gbase[p/64] + 64e + p%64
+    double coalesced = 0;             // diagnostic: share of slot accesses whose lane neighbour is +1
+};
+std::string build_flood_schedule(const ldpc_graph &g, FloodSchedule &s);
+
 // Reference loadFile() semantics (src/alist.cpp:70-93, fixed-width lines).
 std::string load_alist(const char *path, ldpc_graph &g);
 // Row schedule for `threads` threads (multiple of 64, >= M), `cpt` bit slots

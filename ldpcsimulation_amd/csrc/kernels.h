@@ -48,8 +48,19 @@ struct RowSched {
     const uint32_t *vn_info;        // [threads * cpt]
 };
 
+// Device copy of graph.h's FloodSchedule (global-memory flooding kernel).
+struct FloodSched {
+    int M_pad, dc, ngroups, e_pad;
+    const int32_t *sp, *sq;         // [dc * M_pad] slot-major bit position / c2v element
+    const uint8_t *rdeg;            // [M_pad]
+    const int32_t *pos_of_bit;      // [N]
+    const int32_t *bit_at;          // [ngroups * 64]
+    const uint8_t *pdeg;            // [ngroups * 64]
+    const int32_t *gbase;           // [ngroups]
+};
+
 struct KernelChoice {
-    const char *name;               // "rows", "lds" or "global"
+    const char *name;               // "rows", "lds", "flood" or "global"
     int lds_bytes;                  // dynamic LDS per block
     size_t scratch_per_block;       // global kernel
     int threads;
@@ -58,12 +69,14 @@ struct KernelChoice {
 
 // Pick the kernel for a graph / precision. rs (may be null) is the row
 // schedule when the graph admits one; force selects "lds"/"global" for tests.
-KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force = nullptr);
+// fs (may be null): the flood schedule, used for codes whose state exceeds LDS.
+KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force = nullptr,
+                           const FloodSched *fs = nullptr);
 // Launch the decode. gscratch must hold choice.scratch_per_block * grid bytes
 // for the global kernel (grid returned through *grid_out, may be null).
 hipError_t launch_decode(const DevGraph &g, const DecodeArgs &a, bool f64, const KernelChoice &kc,
                          void *gscratch, int gscratch_blocks, hipStream_t s, const RowSched *rs = nullptr,
-                         int num_cus = 256);
+                         int num_cus = 256, const FloodSched *fs = nullptr);
 int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc);
 
 // Exhaustive device check that dividing by alpha through its correctly rounded

@@ -379,6 +379,216 @@ __device__ __forceinline__ float nms_div<float>(float x, float alpha, const Deco
     return x / alpha;
 }
 
+// =====================================================================
+// Global-memory flooding kernel (codes whose state exceeds LDS, DVB-S2).
+//
+// One workgroup per codeword (persistent), the codeword's state in a global
+// scratch slot, laid out by the FloodSchedule so every access is coalesced:
+//   app[NP + 1], yq[NP]     bits in storage order (NP = ngroups*64; app[NP] = +inf)
+//   c2v[e_pad + 64]         edge e of position p at gbase[p/64] + 64e + p%64
+//   m12[M_pad], meta[M_pad] the packed check state, rows in chain order:
+//                           (min1, min2) after /alpha or the offset, and
+//                           argmin | output sign bits << 5
+// Check phase: thread per row (slot-major schedule: lane i reads sp[k*M_pad+i]);
+// the row's last messages are rebuilt from its packed state, the new ones are
+// computed with the reference's comparisons (as cn_exact) and scattered into
+// c2v. Bit phase: thread per position, sum = yq + c2v in nlist order.
+// =====================================================================
+template <typename F> struct F2T;
+template <> struct F2T<float> { using T = float2; };
+template <> struct F2T<double> { using T = double2; };
+
+template <typename F, int SRC, int DC>
+__global__ __launch_bounds__(512, 4) void k_decode_flood(DecodeArgs a, DevGraph g, FloodSched fs, unsigned char *scratch,
+                                                      size_t slot_bytes)
+{
+    using F2 = typename F2T<F>::T;
+    __shared__ int red[32 + 16 * 8];
+    __shared__ unsigned long long acc[6];   // the block's totals (thread 0)
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int N = g.N, NP = fs.ngroups * 64, MP = fs.M_pad;
+    unsigned char *base = scratch + slot_bytes * blockIdx.x;
+    F *app = reinterpret_cast<F *>(base);                       // [NP + 1]
+    F *yq = app + (NP + 1);                                     // [NP]
+    F *c2v = yq + NP;                                           // [e_pad + 64]
+    F2 *m12 = reinterpret_cast<F2 *>(c2v + (fs.e_pad + 64 + 1) / 2 * 2);   // 16-B aligned for double2
+    uint32_t *meta = reinterpret_cast<uint32_t *>(m12 + MP);
+    const F alpha = (F)a.alpha, delta = (F)a.delta;
+
+    if (tid == 0) {
+        app[NP] = dinf<F>();   // sentinel position of padding slots
+#pragma unroll
+        for (int q = 0; q < 6; ++q) acc[q] = 0;
+    }
+
+    for (int b = blockIdx.x; b < a.batch; b += gridDim.x) {
+        const uint64_t cw = a.first_cw + (uint64_t)b;
+        const int8_t *cvec = nullptr;
+        if (SRC == SRC_GIVEN) {
+            if (a.c) cvec = a.c + (size_t)b * N;
+        } else if (a.cw_table) {
+            cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+        }
+        // ---- channel + front-end (:214-238) into storage order ----
+        int unc = 0;
+        if (SRC == SRC_GIVEN) {
+            const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
+            for (int v = tid; v < N; v += nt) {
+                const F q = front_end<F>(y[v], a);
+                const int p = fs.pos_of_bit[v];
+                yq[p] = q;
+                app[p] = q;
+                const int cv = cvec ? cvec[v] : 1;
+                unc += ((q > F(0) ? 1 : -1) * cv < 0);
+            }
+        } else {
+            const F sigma = (F)a.sigma;
+            const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+            for (int g4 = tid; g4 * 4 < N; g4 += nt) {
+                uint32_t u[4];
+                philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                F n[4];
+                box_muller(u[0], u[1], n[0], n[1]);
+                box_muller(u[2], u[3], n[2], n[3]);
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4) {
+                    const int v = g4 * 4 + q4;
+                    if (v < N) {
+                        const int cv = cvec ? cvec[v] : 1;
+                        const F yv = (F)cv * (F(1) + sigma * n[q4]);
+                        if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
+                        const F q = front_end<F>(yv, a);
+                        const int p = fs.pos_of_bit[v];
+                        yq[p] = q;
+                        app[p] = q;
+                        unc += ((q > F(0) ? 1 : -1) * cv < 0);
+                    }
+                }
+            }
+        }
+        for (int i = tid; i < MP; i += nt) {   // c2v_old = +0: v2c = yq on the first pass (:364-370)
+            F2 z;
+            z.x = F(0);
+            z.y = F(0);
+            m12[i] = z;
+            meta[i] = 0;
+        }
+        __syncthreads();
+
+        for (int it = 0; it < a.T; ++it) {
+            // ---- check nodes (:410-450, :494-515) ----
+            for (int i = tid; i < MP; i += nt) {
+                const int deg = fs.rdeg[i];
+                if (deg == 0) continue;
+                int sp[DC];
+#pragma unroll
+                for (int k = 0; k < DC; ++k) sp[k] = k < deg ? fs.sp[(size_t)k * MP + i] : NP;
+                F xa[DC];
+#pragma unroll
+                for (int k = 0; k < DC; ++k) xa[k] = app[sp[k]];
+                const F2 old = m12[i];
+                const uint32_t om = meta[i];
+                const int oidx = (int)(om & 31u);
+                F mn1 = dinf<F>(), mn2 = dinf<F>();
+                int amin = 31;
+                uint32_t sg = 0;
+                F ax[DC];
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    if (k < deg) {
+                        F cold = (k == oidx) ? old.y : old.x;
+                        if ((om >> (5 + k)) & 1u) cold = -cold;
+                        const F x = xa[k] - cold;                     // v2c (:469)
+                        sg |= (uint32_t)(!(x >= F(0))) << k;          // sgn(v2c) < 0 (:518-523)
+                        ax[k] = dabs(x);
+                        if (ax[k] <= mn1) { mn2 = mn1; mn1 = ax[k]; amin = k; }   // :428-433
+                        else if (ax[k] < mn2) { mn2 = ax[k]; }                    // :434-437
+                    }
+                }
+                const uint32_t degmask = (1u << deg) - 1u;
+                uint32_t eff = (__popc(sg) & 1) ? (sg ^ degmask) : sg;   // prod * sgn(v2c_k)
+                F M1 = mn1, M2 = mn2;
+                if (a.variant == V_NMS) {
+                    M1 = nms_div<F>(mn1, alpha, a);               // :498
+                    M2 = nms_div<F>(mn2, alpha, a);
+                } else if (a.variant == V_OMS) {
+                    const F t1 = mn1 - delta, t2 = mn2 - delta;   // :509
+                    const bool p1 = t1 > F(0), p2 = t2 > F(0);
+                    M1 = p1 ? t1 : F(0);
+                    M2 = p2 ? t2 : F(0);
+                    // sgn(c2v) of :511 maps -0.0 to +1; a zeroed message is +0 (:513)
+                    const uint32_t abit = (amin < 31) ? (1u << amin) : 0u;
+                    if (!p1 || mn1 == F(0)) eff &= abit;
+                    if (!p2 || mn2 == F(0)) eff &= ~abit;
+                }
+                F2 nw;
+                nw.x = M1;
+                nw.y = M2;
+                m12[i] = nw;
+                meta[i] = (uint32_t)amin | (eff << 5);
+#pragma unroll
+                for (int k = 0; k < DC; ++k) {
+                    if (k < deg) {
+                        const F mag = (k == amin) ? M2 : M1;
+                        c2v[fs.sq[(size_t)k * MP + i]] = ((eff >> k) & 1u) ? -mag : mag;
+                    }
+                }
+            }
+            __syncthreads();
+            // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
+            for (int p = tid; p < NP; p += nt) {
+                const int d = fs.pdeg[p];
+                if (d == 0) continue;
+                const F *cp = c2v + fs.gbase[p >> 6] + (p & 63);
+                F sum = yq[p];
+                for (int e = 0; e < d; ++e) sum += cp[64 * e];
+                app[p] = sum;
+            }
+            __syncthreads();
+        }
+
+        // ---- decisions, error weight (:270, :382-393), syndrome ----
+        int w = 0, synd = 0;
+        for (int v = tid; v < N; v += nt) {
+            const int d = app[fs.pos_of_bit[v]] > F(0) ? 1 : -1;   // :471-474
+            const int cv = cvec ? cvec[v] : 1;
+            w += (d != cv);
+            if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+        }
+        for (int i = tid; i < MP; i += nt) {
+            const int deg = fs.rdeg[i];
+            int par = 0;
+            for (int k = 0; k < deg; ++k) par ^= (app[fs.sp[(size_t)k * MP + i]] > F(0)) ? 0 : 1;
+            synd |= par;
+        }
+        int sums[3] = {w, unc, synd};
+        block_sum_n<3>(sums, red + 32);
+        if (tid == 0) {
+            const int sf = sums[2] > 0;
+            acc[0] += (unsigned long long)sums[0];
+            acc[1] += (unsigned long long)(sums[0] > 0);
+            acc[2] += (unsigned long long)sums[1];
+            acc[3] += 1ull;
+            acc[5] += (unsigned long long)sf;
+            if (sums[0] > 0 && a.hist) atomicAdd(&a.hist[sums[0] - 1], 1ull);
+            if (a.frame_res) a.frame_res[b] = make_int4(sums[0], sums[1], sf, 0);
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && acc[3] > 0) {
+        acc[4] = acc[3] * (unsigned long long)a.T;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) atomicAdd(&a.counts[q], acc[q]);
+    }
+}
+
+static size_t flood_slot_bytes(const DevGraph &g, const FloodSched &fs, bool f64)
+{
+    const size_t fsz = f64 ? 8 : 4, NP = (size_t)fs.ngroups * 64;
+    const size_t nf = (NP + 1) + NP + ((size_t)fs.e_pad + 64 + 1) / 2 * 2;
+    return (nf * fsz + (size_t)fs.M_pad * (2 * fsz + 4) + 255) & ~(size_t)255;
+}
+
 // s += r for every codeword of a pack (one v_pk_add_f32 for two fp32 codewords).
 template <typename F, int C>
 __device__ __forceinline__ void padd(Pack<F, C> &s, const Pack<F, C> &r)
@@ -954,7 +1164,7 @@ static size_t rows_lds(const DevGraph &g, const RowSched &rs, bool f64, int C)
     return ((size_t)C * ((size_t)g.N + 2 + (size_t)rs.e_pad + 64) * fs + 4 * (32 + 16 * 8) + 15) & ~(size_t)15;
 }
 
-KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force)
+KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, const char *force, const FloodSched *fs)
 {
     KernelChoice kc;
     kc.threads = kThreads;
@@ -962,7 +1172,15 @@ KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, cons
     kc.scratch_per_block = 0;
     const bool want_lds = force && force[0] == 'l';
     const bool want_global = force && force[0] == 'g';
-    if (rs && rs->threads > 0 && !want_lds && !want_global) {
+    const bool want_flood = force && force[0] == 'f';
+    if (fs && fs->M_pad > 0 && fs->dc <= 32 && want_flood) {
+        kc.name = "flood";
+        kc.lds_bytes = 0;
+        kc.threads = 512;
+        kc.scratch_per_block = flood_slot_bytes(g, *fs, f64);
+        return kc;
+    }
+    if (rs && rs->threads > 0 && !want_lds && !want_global && !want_flood) {
         const int C = rows_cw_per_block(f64, rs->dc);
         const size_t lds = rows_lds(g, *rs, f64, C);
         if (lds <= kMaxLds) {
@@ -974,9 +1192,14 @@ KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, cons
         }
     }
     const size_t lds = (state_bytes(g, f64) + 64 + 15) & ~(size_t)15;
-    if (lds <= kMaxLds && !want_global) {
+    if (lds <= kMaxLds && !want_global && !want_flood) {
         kc.name = "lds";
         kc.lds_bytes = (int)lds;
+    } else if (fs && fs->M_pad > 0 && fs->dc <= 32 && !want_global) {
+        kc.name = "flood";
+        kc.lds_bytes = 0;
+        kc.threads = 512;
+        kc.scratch_per_block = flood_slot_bytes(g, *fs, f64);
     } else {
         kc.name = "global";
         kc.lds_bytes = 0;
@@ -1050,10 +1273,36 @@ static hipError_t launch_rows_dc(const DevGraph &g, const RowSched &rs, const De
     return hipErrorInvalidValue;
 }
 
+template <typename F, int SRC>
+static hipError_t launch_flood_t(const DevGraph &g, const FloodSched &fs, const DecodeArgs &a,
+                                 const KernelChoice &kc, void *gs, int gblocks, hipStream_t s)
+{
+    const int grid = gblocks < a.batch ? gblocks : a.batch;
+    if (fs.dc <= 8)
+        hipLaunchKernelGGL((k_decode_flood<F, SRC, 8>), dim3(grid), dim3(kc.threads), 0, s, a, g, fs,
+                           (unsigned char *)gs, kc.scratch_per_block);
+    else if (fs.dc <= 16)
+        hipLaunchKernelGGL((k_decode_flood<F, SRC, 16>), dim3(grid), dim3(kc.threads), 0, s, a, g, fs,
+                           (unsigned char *)gs, kc.scratch_per_block);
+    else
+        hipLaunchKernelGGL((k_decode_flood<F, SRC, 32>), dim3(grid), dim3(kc.threads), 0, s, a, g, fs,
+                           (unsigned char *)gs, kc.scratch_per_block);
+    return hipGetLastError();
+}
+
 hipError_t launch_decode(const DevGraph &g, const DecodeArgs &a, bool f64, const KernelChoice &kc,
-                         void *gscratch, int gscratch_blocks, hipStream_t s, const RowSched *rs, int num_cus)
+                         void *gscratch, int gscratch_blocks, hipStream_t s, const RowSched *rs, int num_cus,
+                         const FloodSched *fs)
 {
     if (a.batch <= 0) return hipSuccess;
+    if (kc.name[0] == 'f') {
+        if (!fs) return hipErrorInvalidValue;
+        if (f64)
+            return a.src == SRC_GIVEN ? launch_flood_t<double, SRC_GIVEN>(g, *fs, a, kc, gscratch, gscratch_blocks, s)
+                                      : launch_flood_t<double, SRC_PHILOX>(g, *fs, a, kc, gscratch, gscratch_blocks, s);
+        return a.src == SRC_GIVEN ? launch_flood_t<float, SRC_GIVEN>(g, *fs, a, kc, gscratch, gscratch_blocks, s)
+                                  : launch_flood_t<float, SRC_PHILOX>(g, *fs, a, kc, gscratch, gscratch_blocks, s);
+    }
     if (kc.name[0] == 'r') {
         if (!rs) return hipErrorInvalidValue;
         if (f64)
@@ -1082,6 +1331,10 @@ int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc)
                                                      : (const void *)k_decode_rows<float, SRC_PHILOX, 1, 16, 4, 2>);
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kc.lds_bytes);
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads, kc.lds_bytes);
+    } else if (kc.name[0] == 'f') {
+        const void *fn = f64 ? (const void *)k_decode_flood<double, SRC_PHILOX, 8>
+                             : (const void *)k_decode_flood<float, SRC_PHILOX, 8>;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads, 0);
     } else if (kc.lds_bytes > 0) {
         const void *fn = f64 ? (const void *)k_decode_lds<double, SRC_PHILOX> : (const void *)k_decode_lds<float, SRC_PHILOX>;
         (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kc.lds_bytes);

@@ -157,11 +157,12 @@ def test_sim_independent_of_batch_split(gpu_ctx_factory):
 
 @pytest.mark.parametrize("code", CODES)
 def test_all_kernels_bit_identical(monkeypatch, code):
-    """The row-parallel, per-codeword-LDS and global-memory kernels give identical results."""
+    """The row-parallel, per-codeword-LDS, flood (global, coalesced) and generic global kernels give
+    identical results."""
     native = _native()
     g = native.Graph.from_alist(code_path(code))
     ctxs = {}
-    for k in ("default", "lds", "global"):
+    for k in ("default", "lds", "flood", "global"):
         if k == "default":
             monkeypatch.delenv("LDPC_KERNEL", raising=False)
         else:
@@ -174,7 +175,7 @@ def test_all_kernels_bit_identical(monkeypatch, code):
     for cfg, prec in ((c, p) for c in cfgs for p in (native.F32, native.F64)):
         cfg.precision = prec
         names = {k: c.kernel_info(cfg)["kernel"] for k, c in ctxs.items()}
-        assert names["lds"] == "lds" and names["global"] == "global"
+        assert names["lds"] == "lds" and names["global"] == "global" and names["flood"] == "flood"
         if code != "4000.2000.4.244.alist":
             assert names["default"] == "rows"
         outs = {k: c.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300) for k, c in ctxs.items()}
@@ -291,3 +292,18 @@ def test_signed_zeros_and_ties_exact(vname):
         d, fr, cnt = ctx.decode(y, cfg)
         want = A.decode(y, T, O.Cfg(**v))
         assert int((d != want).sum()) == 0, T
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_dvbs2_flood_decisions_vs_oracle(gpu_ctx_factory, prec):
+    """DVB-S2 N=64800 (state beyond LDS: the flood kernel) -- decisions equal the oracle's."""
+    native = _native()
+    ctx = gpu_ctx_factory("dvbs2_1_2.alist", 64)
+    f32 = prec == "f32"
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=6, precision=native.F32 if f32 else native.F64)
+    assert ctx.kernel_info(cfg)["kernel"] == "flood"
+    y, d, fr, cnt = ctx.sim_trace(0.8, 0.5, cfg, seed=5, stream_id=1, first_cw=3, batch=3)
+    A = O.Alist(code_path("dvbs2_1_2.alist"))
+    want = A.decode(y, 6, O.Cfg(variant=1, alpha=1.25))
+    assert int((d != want).sum()) == 0
+    assert np.array_equal(fr["bit_err"], (want != 1).sum(axis=1))
