@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 1
+#define LDPC_ABI_VERSION 2
 
 typedef enum {
     LDPC_OK = 0,
@@ -60,6 +60,14 @@ typedef enum { LDPC_MS = 0, LDPC_NMS = 1, LDPC_OMS = 2 } ldpc_variant;
 /* Message arithmetic. F64 is the reference's own precision and reproduces
  * its decisions bit-for-bit for identical y; F32 is the throughput path. */
 typedef enum { LDPC_F32 = 0, LDPC_F64 = 1 } ldpc_precision;
+
+/* Message-passing schedule. FLOODING is the reference's (all check nodes,
+ * then all bit nodes: src/decodeMinSum.cpp:247-263). LAYERED is the
+ * row-serial schedule of SURVEY §8(f) row 2 (BASELINE config 3; no
+ * reference counterpart): rows in the order ldpc_graph_layers() returns,
+ * each row updating the posteriors of its bits in place, bit-disjoint rows
+ * of a layer in parallel. */
+typedef enum { LDPC_FLOODING = 0, LDPC_LAYERED = 1 } ldpc_schedule;
 
 typedef struct ldpc_graph ldpc_graph;
 typedef struct ldpc_ctx ldpc_ctx;
@@ -93,6 +101,8 @@ typedef struct {
     double  ymax;       /* Ymax                                             */
     double  alpha;      /* NMS divisor                                      */
     double  delta;      /* OMS offset                                       */
+    int32_t schedule;   /* ldpc_schedule (ABI 2)                            */
+    int32_t reserved;   /* 0                                                */
 } ldpc_decoder_cfg;
 
 int         ldpc_abi_version(void);
@@ -110,6 +120,11 @@ int  ldpc_graph_create(int N, int M, const int *num_nlist, const int *const *nli
 int  ldpc_graph_load_alist(const char *path, ldpc_graph **out);
 int  ldpc_graph_info(const ldpc_graph *g, int *N, int *M, int *E, int *maxdv, int *maxdc);
 void ldpc_graph_destroy(ldpc_graph *g);
+/* Row order and layer partition of the LAYERED schedule: row_order[M] lists
+ * the rows in serial order, layer_ptr[nlayers+1] delimits the layers (runs
+ * of rows that share no bit). Either array may be NULL (query nlayers
+ * first). No reference counterpart. */
+int  ldpc_graph_layers(const ldpc_graph *g, int32_t *row_order, int32_t *layer_ptr, int *nlayers);
 
 /* ---- device context --------------------------------------------------- */
 int  ldpc_device_count(int *n);

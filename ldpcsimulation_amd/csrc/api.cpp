@@ -83,6 +83,9 @@ struct ldpc_ctx {
     bool has_fs = false;
     ldpc::FloodSched fs{};
     DevBuf fsched;                                        // flood kernel schedule (codes beyond LDS)
+    bool has_ls = false;
+    ldpc::LayerSched ls{};                                // layered schedule (row order = fs order)
+    DevBuf lsched;
     DevBuf divcheck;                                      // mismatch counter of verify_div_by_reciprocal
     std::vector<std::pair<float, bool>> div_ok;           // alpha -> reciprocal division exact
 };
@@ -150,6 +153,27 @@ int ldpc_graph_info(const ldpc_graph *g, int *N, int *M, int *E, int *maxdv, int
 
 void ldpc_graph_destroy(ldpc_graph *g) { delete g; }
 
+int ldpc_graph_layers(const ldpc_graph *g, int32_t *row_order, int32_t *layer_ptr, int *nlayers)
+{
+    if (!g || !nlayers) return set_err(LDPC_ERR_INVALID, "null argument");
+    ldpc::FloodSchedule fh;
+    ldpc::LayerSchedule lh;
+    std::string err;
+    try {
+        err = ldpc::build_flood_schedule(*g, fh);
+        if (err.empty()) err = ldpc::build_layers(*g, fh, lh);
+    } catch (const std::bad_alloc &) {
+        return set_err(LDPC_ERR_NOMEM, "layer schedule out of memory");
+    }
+    if (!err.empty()) return set_err(LDPC_ERR_GRAPH, "%s", err.c_str());
+    *nlayers = (int)lh.lptr.size() - 1;
+    if (row_order)
+        for (int i = 0; i < g->M; ++i) row_order[i] = lh.row_order[i];
+    if (layer_ptr)
+        for (size_t L = 0; L < lh.lptr.size(); ++L) layer_ptr[L] = lh.lptr[L];
+    return LDPC_OK;
+}
+
 // ----------------------------------------------------------------- context
 int ldpc_device_count(int *n)
 {
@@ -171,7 +195,7 @@ static void ctx_free(ldpc_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->graph, &c->counts, &c->hist, &c->y_stage, &c->c_stage, &c->d_stage, &c->fw_stage,
-                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck, &c->fsched})
+                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck, &c->fsched, &c->lsched})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -316,6 +340,24 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
             c->fs.pdeg = (const uint8_t *)(fb + o_pd);
             c->fs.gbase = (const int32_t *)(fb + o_gb);
             c->has_fs = true;
+            ldpc::LayerSchedule lh;
+            if (fh.dc <= ldpc::kPackedMaxDc && ldpc::build_layers(*g, fh, lh).empty()) {
+                const size_t n_lp = lh.lptr.size(), n_sp = lh.sp.size(), n_rd = lh.rdeg.size();
+                const size_t o_sp = al(4 * n_lp), o_rd = o_sp + al(4 * n_sp), tot = o_rd + al(n_rd);
+                CTX_TRY(c->lsched.ensure(tot));
+                unsigned char *lb = (unsigned char *)c->lsched.p;
+                CTX_TRY(hipMemcpy(lb, lh.lptr.data(), 4 * n_lp, hipMemcpyHostToDevice));
+                CTX_TRY(hipMemcpy(lb + o_sp, lh.sp.data(), 4 * n_sp, hipMemcpyHostToDevice));
+                CTX_TRY(hipMemcpy(lb + o_rd, lh.rdeg.data(), n_rd, hipMemcpyHostToDevice));
+                c->ls.nlayers = (int)n_lp - 1;
+                c->ls.M_pad = lh.M_pad;
+                c->ls.lptr = (const int32_t *)lb;
+                c->ls.sp = (const int32_t *)(lb + o_sp);
+                c->ls.rdeg = (const uint8_t *)(lb + o_rd);
+                for (int L = 0; L < c->ls.nlayers; ++L)
+                    c->ls.max_layer = std::max(c->ls.max_layer, lh.lptr[L + 1] - lh.lptr[L]);
+                c->has_ls = true;
+            }
         }
     }
     CTX_TRY(c->counts.ensure(8 * sizeof(unsigned long long)));
@@ -367,7 +409,11 @@ static int check_cfg(const ldpc_ctx *c, const ldpc_decoder_cfg *cfg)
     if ((cfg->quantize || cfg->saturate) && !(cfg->ymax > 0))
         return set_err(LDPC_ERR_INVALID, "quantize/saturate need ymax > 0");
     if (cfg->quantize && (cfg->qbits < 1 || cfg->qbits > 30)) return set_err(LDPC_ERR_INVALID, "qbits out of range");
-    (void)c;
+    if (cfg->schedule != LDPC_FLOODING && cfg->schedule != LDPC_LAYERED)
+        return set_err(LDPC_ERR_INVALID, "bad schedule %d", cfg->schedule);
+    if (cfg->schedule == LDPC_LAYERED && !c->has_ls)
+        return set_err(LDPC_ERR_UNSUPPORTED, "layered schedule unavailable for this graph (row degree > %d)",
+                       ldpc::kPackedMaxDc);
     return LDPC_OK;
 }
 
@@ -418,14 +464,32 @@ static int nms_setup(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, ldpc::DecodeArgs 
     return LDPC_OK;
 }
 
-static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64)
+static ldpc::KernelChoice select_kernel(const ldpc_ctx *c, bool f64, int schedule)
 {
-    const ldpc::KernelChoice kc =
-        ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr,
-                            c->has_fs ? &c->fs : nullptr);
-    int gblocks = 0;
+    if (schedule == LDPC_LAYERED)
+        return ldpc::choose_layered(c->dg, f64, c->fs, c->ls, c->force[0] ? c->force : nullptr);
+    return ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr,
+                               c->has_fs ? &c->fs : nullptr);
+}
+
+static bool is_layered(const ldpc::KernelChoice &kc) { return kc.name[0] == 'l' && kc.name[1] == 'a'; }
+
+static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int schedule)
+{
+    const ldpc::KernelChoice kc = select_kernel(c, f64, schedule);
+    const bool layered = is_layered(kc);
+    int gblocks = layered ? c->num_cus : 0;
     if (kc.scratch_per_block) {
-        int per_cu = ldpc::blocks_per_cu(c->dg, f64, kc);
+        int per_cu = layered ? ldpc::layered_blocks_per_cu(f64, kc) : ldpc::blocks_per_cu(c->dg, f64, kc);
+        // Global layered kernel: one codeword per CU by default, so the
+        // resident state (DVB-S2: 256 x 583 KB) stays inside the 256 MiB
+        // Infinity Cache (2 per CU measured 1.5x slower); LDPC_LAYERED_BPC
+        // overrides (experiments).
+        if (layered) {
+            int want = 1;
+            if (const char *e = std::getenv("LDPC_LAYERED_BPC")) want = std::max(1, std::atoi(e));
+            per_cu = std::min(per_cu, want);
+        }
         if (per_cu <= 0) per_cu = 1;
         gblocks = per_cu * c->num_cus;
         if (gblocks > a.batch) gblocks = a.batch;
@@ -444,8 +508,11 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64)
 #define a as
 #endif
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream, c->has_rs ? &c->rs : nullptr,
-                                c->num_cus, c->has_fs ? &c->fs : nullptr));
+    if (layered)
+        HIP_TRY(ldpc::launch_layered(c->dg, a, f64, kc, c->fs, c->ls, c->gscratch.p, gblocks, c->stream));
+    else
+        HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream,
+                                    c->has_rs ? &c->rs : nullptr, c->num_cus, c->has_fs ? &c->fs : nullptr));
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
 #ifdef LDPC_STAMPS
@@ -546,7 +613,7 @@ int ldpc_decode_batch(ldpc_ctx *c, const void *y, int batch, const ldpc_decoder_
     ldpc_counts before;
     rc = read_counts(c, &before, 0);
     if (rc) return rc;
-    rc = run_kernel(c, a, f64);
+    rc = run_kernel(c, a, f64, cfg->schedule);
     if (rc) return rc;
     if (d_host) HIP_TRY(hipMemcpyAsync(d_out, c->d_stage.p, nbytes, hipMemcpyDeviceToHost, c->stream));
     if (w_host)
@@ -616,7 +683,7 @@ static int sim_launch_impl(ldpc_ctx *c, double ebn0_db, double R, const ldpc_dec
     a.frame_res = (int4 *)frames_dev;
     a.y_out = y_out_dev;
     a.d_out = d_out_dev;
-    return run_kernel(c, a, cfg->precision == LDPC_F64);
+    return run_kernel(c, a, cfg->precision == LDPC_F64, cfg->schedule);
 }
 
 int ldpc_sim_launch(ldpc_ctx *c, double ebn0_db, double R, const ldpc_decoder_cfg *cfg, uint64_t seed,
@@ -730,12 +797,13 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     if (!c || !cfg) return set_err(LDPC_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     const bool f64 = cfg->precision == LDPC_F64;
-    const ldpc::KernelChoice kc =
-        ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr,
-                            c->has_fs ? &c->fs : nullptr);
+    int rc = check_cfg(c, cfg);
+    if (rc) return rc;
+    const ldpc::KernelChoice kc = select_kernel(c, f64, cfg->schedule);
     if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", kc.name);
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
-    if (bpc) *bpc = ldpc::blocks_per_cu(c->dg, f64, kc);
+    if (bpc) *bpc = is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
+                                   : ldpc::blocks_per_cu(c->dg, f64, kc);
     return LDPC_OK;
 }
 

@@ -385,6 +385,8 @@ std::string build_flood_schedule(const ldpc_graph &g, FloodSchedule &s)
             qpos[(size_t)j * dcs + k] = s.gbase[p / 64] + 64 * e + (p % 64);
         }
     }
+    s.chain_head.assign(M, 1);
+    for (int i = 1; i < M; ++i) s.chain_head[i] = rnext[rorder[i - 1]] == rorder[i] ? 0 : 1;
     s.M_pad = (M + 63) / 64 * 64;
     s.row_of.assign(s.M_pad, -1);
     s.rdeg.assign(s.M_pad, 0);
@@ -408,6 +410,54 @@ std::string build_flood_schedule(const ldpc_graph &g, FloodSchedule &s)
         }
     }
     s.coalesced = tot ? (double)coal / (double)tot : 0.0;
+    return "";
+}
+
+std::string build_layers(const ldpc_graph &g, const FloodSchedule &s, LayerSchedule &ls)
+{
+    ls = LayerSchedule();
+    const int M = g.M, N = g.N;
+    if ((int)s.row_of.size() < M) return "flood schedule missing";
+    const int dcs = std::max(g.maxdc, 1);
+    // first-fit colouring in chain order
+    std::vector<std::vector<int32_t>> bit_layers(N);
+    std::vector<int32_t> layer_of(M, -1), forbid;
+    int nlayers = 0;
+    for (int i = 0; i < M; ++i) {
+        const int j = s.row_of[i];
+        if (j < 0) return "padding inside the row order";
+        const int32_t *rc = &g.row_cols[(size_t)j * dcs];
+        forbid.clear();
+        for (int k = 0; k < g.row_deg[j]; ++k)
+            for (int32_t L : bit_layers[rc[k]]) forbid.push_back(L);
+        std::sort(forbid.begin(), forbid.end());
+        int L = 0;
+        for (int32_t f : forbid) {
+            if (f == L) ++L;
+            else if (f > L) break;
+        }
+        layer_of[i] = L;
+        nlayers = std::max(nlayers, L + 1);
+        for (int k = 0; k < g.row_deg[j]; ++k) bit_layers[rc[k]].push_back(L);
+    }
+    // layered order: layer by layer, chain order inside a layer
+    std::vector<int32_t> cnt(nlayers + 1, 0), pos_i(M);
+    for (int i = 0; i < M; ++i) ++cnt[layer_of[i] + 1];
+    for (int L = 0; L < nlayers; ++L) cnt[L + 1] += cnt[L];
+    ls.lptr = cnt;
+    for (int i = 0; i < M; ++i) pos_i[cnt[layer_of[i]]++] = i;
+    ls.dc = s.dc;
+    ls.M_pad = (M + 63) / 64 * 64;
+    const int NP = s.ngroups * 64;
+    ls.row_order.assign(M, -1);
+    ls.rdeg.assign(ls.M_pad, 0);
+    ls.sp.assign((size_t)ls.dc * ls.M_pad, NP);
+    for (int n = 0; n < M; ++n) {
+        const int i = pos_i[n];
+        ls.row_order[n] = s.row_of[i];
+        ls.rdeg[n] = s.rdeg[i];
+        for (int k = 0; k < s.dc; ++k) ls.sp[(size_t)k * ls.M_pad + n] = s.sp[(size_t)k * s.M_pad + i];
+    }
     return "";
 }
 

@@ -63,6 +63,7 @@ struct FloodSchedule {
     int dc = 0;                       // max row degree
     int ngroups = 0, e_pad = 0;       // 64-bit groups of the c2v layout, its size
     std::vector<int32_t> row_of;      // [M_pad] check row at order position i (-1: padding)
+    std::vector<uint8_t> chain_head;  // [M] 1 where order position i starts a row chain
     std::vector<uint8_t> rdeg;        // [M_pad]
     std::vector<int32_t> sp;          // [dc * M_pad] slot-major: bit position (storage order) of slot k (pads: ngroups*64, the +inf sentinel)
     std::vector<int32_t> sq;          // [dc * M_pad] slot-major: c2v element of slot k (pads: e_pad + i%64)
@@ -73,6 +74,24 @@ struct FloodSchedule {
     double coalesced = 0;             // diagnostic: share of slot accesses whose lane neighbour is +1
 };
 std::string build_flood_schedule(const ldpc_graph &g, FloodSchedule &s);
+
+// Layered schedule (kernels.hip, k_decode_layered_*): rows grouped into
+// layers of rows that share no bit, by first-fit colouring in the flood
+// schedule's chain order (each row joins the lowest layer none of its bits
+// is in yet), so a quasi-cyclic block row stays together and rows keep
+// their chain neighbours (coalesced gathers). The serial row order is
+// layer by layer, each layer in chain order; updating a layer's rows in
+// parallel equals updating them serially in that order (bit-disjoint rows
+// commute), which is the oracle's row-serial definition.
+struct LayerSchedule {
+    int M_pad = 0, dc = 0;
+    std::vector<int32_t> row_order;   // [M] check row at layered position n
+    std::vector<int32_t> lptr;        // [nlayers + 1] layered positions of each layer
+    std::vector<int32_t> sp;          // [dc * M_pad] slot-major storage position (FloodSchedule order) of
+                                      // edge k of the row at layered position n (pads: the +inf sentinel)
+    std::vector<uint8_t> rdeg;        // [M_pad]
+};
+std::string build_layers(const ldpc_graph &g, const FloodSchedule &s, LayerSchedule &ls);
 
 // Reference loadFile() semantics (src/alist.cpp:70-93, fixed-width lines).
 std::string load_alist(const char *path, ldpc_graph &g);

@@ -59,6 +59,14 @@ struct FloodSched {
     const int32_t *gbase;           // [ngroups]
 };
 
+// Device copy of graph.h's LayerSchedule.
+struct LayerSched {
+    int nlayers = 0, max_layer = 0, M_pad = 0;
+    const int32_t *lptr = nullptr;  // [nlayers + 1] layered row positions of each layer
+    const int32_t *sp = nullptr;    // [dc * M_pad] slot-major storage positions (fs order of bits)
+    const uint8_t *rdeg = nullptr;  // [M_pad]
+};
+
 struct KernelChoice {
     const char *name;               // "rows", "lds", "flood" or "global"
     int lds_bytes;                  // dynamic LDS per block
@@ -78,6 +86,19 @@ hipError_t launch_decode(const DevGraph &g, const DecodeArgs &a, bool f64, const
                          void *gscratch, int gscratch_blocks, hipStream_t s, const RowSched *rs = nullptr,
                          int num_cus = 256, const FloodSched *fs = nullptr);
 int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc);
+
+// Layered schedule (k_decode_layered_*): state in LDS when it fits
+// ("layered_lds"), else in a global slot per block ("layered_global").
+// Requires the flood schedule (row order, storage order) and row degree <= kPackedMaxDc.
+KernelChoice choose_layered(const DevGraph &g, bool f64, const FloodSched &fs, const LayerSched &ls,
+                            const char *force = nullptr);
+hipError_t launch_layered(const DevGraph &g, const DecodeArgs &a, bool f64, const KernelChoice &kc,
+                          const FloodSched &fs, const LayerSched &ls, void *gscratch, int gscratch_blocks,
+                          hipStream_t s);
+int layered_blocks_per_cu(bool f64, const KernelChoice &kc);
+// Packed check state of the flood and layered kernels: a 5-bit argmin and one
+// sign bit per edge in a 32-bit meta word.
+constexpr int kPackedMaxDc = 26;
 
 // Exhaustive device check that dividing by alpha through its correctly rounded
 // reciprocal plus one FMA correction step reproduces IEEE x/alpha for all

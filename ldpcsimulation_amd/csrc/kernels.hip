@@ -589,6 +589,278 @@ static size_t flood_slot_bytes(const DevGraph &g, const FloodSched &fs, bool f64
     return (nf * fsz + (size_t)fs.M_pad * (2 * fsz + 4) + 255) & ~(size_t)255;
 }
 
+// =====================================================================
+// Layered (row-serial) min-sum -- SURVEY §8(f) row 2, BASELINE config 3.
+// The reference only floods (src/decodeMinSum.cpp:247-263); this is the
+// row-serial schedule of the same check-node rule (:410-450, :494-515),
+// restated in oracle/ldpc_oracle.c (orc_decode_layered_*):
+//   x_k = app[b_k] - c2v_old_k;  c2v_k = rule(x);  app[b_k] = x_k + c2v_k
+// row by row in the flood schedule's chain order. Consecutive rows that share
+// no bit commute exactly, so each layer (LayerSched: maximal bit-disjoint runs
+// of chain-order rows; DVB-S2 N=64800: 90 layers of 360 rows) is updated by
+// all its rows at once, one thread per row, with a workgroup barrier between
+// layers. One workgroup per codeword (persistent over the batch). State:
+//   app[NP + 1]            posteriors in storage order (app[NP] = +inf pad)
+//   m12[M_pad], meta[M_pad] the packed check state as in k_decode_flood
+// -- in LDS when it fits (k_decode_layered_lds) or in a per-workgroup global
+// slot (k_decode_layered_global: DVB-S2's 583 KB). No yq and no E-sized
+// message array: a row's old messages are rebuilt from its packed state.
+// =====================================================================
+template <typename F, int SRC>
+__device__ __forceinline__ int channel_to_storage(const DecodeArgs &a, const DevGraph &g, const FloodSched &fs,
+                                                  int b, const int8_t *cvec, F *app)
+{
+    const int tid = threadIdx.x, nt = blockDim.x, N = g.N;
+    const uint64_t cw = a.first_cw + (uint64_t)b;
+    int unc = 0;
+    if (SRC == SRC_GIVEN) {
+        const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
+        for (int v = tid; v < N; v += nt) {
+            const F q = front_end<F>(y[v], a);
+            app[fs.pos_of_bit[v]] = q;
+            const int cv = cvec ? cvec[v] : 1;
+            unc += ((q > F(0) ? 1 : -1) * cv < 0);
+        }
+    } else {
+        const F sigma = (F)a.sigma;
+        const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+        for (int g4 = tid; g4 * 4 < N; g4 += nt) {
+            uint32_t u[4];
+            philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+            F n[4];
+            box_muller(u[0], u[1], n[0], n[1]);
+            box_muller(u[2], u[3], n[2], n[3]);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int v = g4 * 4 + q4;
+                if (v < N) {
+                    const int cv = cvec ? cvec[v] : 1;
+                    const F yv = (F)cv * (F(1) + sigma * n[q4]);
+                    if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
+                    const F q = front_end<F>(yv, a);
+                    app[fs.pos_of_bit[v]] = q;
+                    unc += ((q > F(0) ? 1 : -1) * cv < 0);
+                }
+            }
+        }
+    }
+    return unc;
+}
+
+// One check row of the layered schedule: xs[k] = app of its bits on entry,
+// the updated posteriors x_k + c2v_k on exit; returns the new packed meta
+// (argmin | sign bits << 5) and the new minima in nw. The check-node rule is
+// the reference's (checkNodeUpdates :410-450, applyNormalization :494-499,
+// applyOffset :503-515), as in k_decode_flood.
+template <typename F, int DC>
+__device__ __forceinline__ uint32_t layered_row(const DecodeArgs &a, int deg, typename F2T<F>::T old, uint32_t om,
+                                                F (&xs)[DC], F alpha, F delta, typename F2T<F>::T &nw)
+{
+    const int oidx = (int)(om & 31u);
+    F mn1 = dinf<F>(), mn2 = dinf<F>();
+    int amin = 31;
+    uint32_t sg = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k < deg) {
+            F cold = (k == oidx) ? old.y : old.x;
+            if ((om >> (5 + k)) & 1u) cold = -cold;
+            xs[k] = xs[k] - cold;                           // v2c (:469)
+            sg |= (uint32_t)(!(xs[k] >= F(0))) << k;        // sgn(v2c) < 0 (:518-523)
+            const F ax = dabs(xs[k]);
+            if (ax <= mn1) { mn2 = mn1; mn1 = ax; amin = k; }   // :428-433
+            else if (ax < mn2) { mn2 = ax; }                    // :434-437
+        }
+    }
+    const uint32_t degmask = (1u << deg) - 1u;
+    uint32_t eff = (__popc(sg) & 1) ? (sg ^ degmask) : sg;   // prod * sgn(v2c_k)
+    F M1 = mn1, M2 = mn2;
+    if (a.variant == V_NMS) {
+        M1 = nms_div<F>(mn1, alpha, a);                   // :498
+        M2 = nms_div<F>(mn2, alpha, a);
+    } else if (a.variant == V_OMS) {
+        const F t1 = mn1 - delta, t2 = mn2 - delta;       // :509
+        const bool p1 = t1 > F(0), p2 = t2 > F(0);
+        M1 = p1 ? t1 : F(0);
+        M2 = p2 ? t2 : F(0);
+        // sgn(c2v) of :511 maps -0.0 to +1; a zeroed message is +0 (:513)
+        const uint32_t abit = (amin < 31) ? (1u << amin) : 0u;
+        if (!p1 || mn1 == F(0)) eff &= abit;
+        if (!p2 || mn2 == F(0)) eff &= ~abit;
+    }
+    nw.x = M1;
+    nw.y = M2;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k < deg) {
+            const F mag = (k == amin) ? M2 : M1;
+            xs[k] = xs[k] + (((eff >> k) & 1u) ? -mag : mag);
+        }
+    }
+    return (uint32_t)amin | (eff << 5);
+}
+
+template <typename F, int SRC, int DC, int R>
+__device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const DevGraph &g, const FloodSched &fs,
+                                                  const LayerSched &ls, int b, F *app,
+                                                  typename F2T<F>::T *m12, uint32_t *meta, int *red,
+                                                  unsigned long long *acc)
+{
+    using F2 = typename F2T<F>::T;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int N = g.N, NP = fs.ngroups * 64, MP = ls.M_pad;
+    const F alpha = (F)a.alpha, delta = (F)a.delta;
+    const uint64_t cw = a.first_cw + (uint64_t)b;
+    const int8_t *cvec = nullptr;
+    if (SRC == SRC_GIVEN) {
+        if (a.c) cvec = a.c + (size_t)b * N;
+    } else if (a.cw_table) {
+        cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+    }
+    // ---- channel + front-end (:214-238): app = yq in storage order ----
+    const int unc = channel_to_storage<F, SRC>(a, g, fs, b, cvec, app);
+    for (int i = tid; i < MP; i += nt) {   // c2v_old = +0 (:364-370)
+        F2 z;
+        z.x = F(0);
+        z.y = F(0);
+        m12[i] = z;
+        meta[i] = 0;
+    }
+    __syncthreads();
+
+    for (int it = 0; it < a.T; ++it) {
+        for (int L = 0; L < ls.nlayers; ++L) {
+            const int r1 = ls.lptr[L + 1];
+            // R rows per thread per pass: every gather of the pass is issued
+            // before the first row is computed (one memory round trip per pass)
+            for (int i0 = ls.lptr[L] + tid; i0 < r1; i0 += nt * R) {
+                int deg[R], sp[R][DC];
+                F xs[R][DC];
+                F2 old[R];
+                uint32_t om[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) deg[r] = (i0 + r * nt < r1) ? ls.rdeg[i0 + r * nt] : 0;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) sp[r][k] = k < deg[r] ? ls.sp[(size_t)k * MP + i0 + r * nt] : NP;
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) xs[r][k] = app[sp[r][k]];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (deg[r]) {
+                        old[r] = m12[i0 + r * nt];
+                        om[r] = meta[i0 + r * nt];
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (deg[r]) {
+                        F2 nw;
+                        const uint32_t nm = layered_row<F, DC>(a, deg[r], old[r], om[r], xs[r], alpha, delta, nw);
+                        m12[i0 + r * nt] = nw;
+                        meta[i0 + r * nt] = nm;
+#pragma unroll
+                        for (int k = 0; k < DC; ++k)
+                            if (k < deg[r]) app[sp[r][k]] = xs[r][k];   // posterior update
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+
+    // ---- decisions, error weight (:270, :382-393), syndrome ----
+    int w = 0, synd = 0;
+    for (int v = tid; v < N; v += nt) {
+        const int d = app[fs.pos_of_bit[v]] > F(0) ? 1 : -1;   // :471-474
+        const int cv = cvec ? cvec[v] : 1;
+        w += (d != cv);
+        if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+    }
+    for (int i = tid; i < MP; i += nt) {
+        const int deg = ls.rdeg[i];
+        int par = 0;
+        for (int k = 0; k < deg; ++k) par ^= (app[ls.sp[(size_t)k * MP + i]] > F(0)) ? 0 : 1;
+        synd |= par;
+    }
+    int sums[3] = {w, unc, synd};
+    block_sum_n<3>(sums, red);
+    if (tid == 0) {
+        const int sf = sums[2] > 0;
+        acc[0] += (unsigned long long)sums[0];
+        acc[1] += (unsigned long long)(sums[0] > 0);
+        acc[2] += (unsigned long long)sums[1];
+        acc[3] += 1ull;
+        acc[5] += (unsigned long long)sf;
+        if (sums[0] > 0 && a.hist) atomicAdd(&a.hist[sums[0] - 1], 1ull);
+        if (a.frame_res) a.frame_res[b] = make_int4(sums[0], sums[1], sf, 0);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void flush_acc(const DecodeArgs &a, unsigned long long *acc)
+{
+    if (threadIdx.x == 0 && acc[3] > 0) {
+        acc[4] = acc[3] * (unsigned long long)a.T;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) atomicAdd(&a.counts[q], acc[q]);
+    }
+}
+
+// LDS offsets of the layered state: app[NP + 1] | pad | m12[M_pad] | meta[M_pad].
+__host__ __device__ inline size_t layered_m12_off(const FloodSched &fs, size_t fsz)
+{
+    return (((size_t)fs.ngroups * 64 + 1) * fsz + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t layered_state_bytes(const FloodSched &fs, const LayerSched &ls, size_t fsz)
+{
+    return (layered_m12_off(fs, fsz) + (size_t)ls.M_pad * (2 * fsz + 4) + 255) & ~(size_t)255;
+}
+
+template <typename F, int SRC, int DC, int R>
+__global__ __launch_bounds__(512) void k_decode_layered_lds(DecodeArgs a, DevGraph g, FloodSched fs, LayerSched ls)
+{
+    using F2 = typename F2T<F>::T;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int red[16 * 4];
+    __shared__ unsigned long long acc[6];
+    F *app = reinterpret_cast<F *>(smem);
+    F2 *m12 = reinterpret_cast<F2 *>(smem + layered_m12_off(fs, sizeof(F)));
+    uint32_t *meta = reinterpret_cast<uint32_t *>(m12 + ls.M_pad);
+    if (threadIdx.x == 0) {
+        app[fs.ngroups * 64] = dinf<F>();
+#pragma unroll
+        for (int q = 0; q < 6; ++q) acc[q] = 0;
+    }
+    for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
+        decode_layered_cw<F, SRC, DC, R>(a, g, fs, ls, b, app, m12, meta, red, acc);
+    flush_acc(a, acc);
+}
+
+template <typename F, int SRC, int DC, int R>
+__global__ __launch_bounds__(512) void k_decode_layered_global(DecodeArgs a, DevGraph g, FloodSched fs, LayerSched ls,
+                                                               unsigned char *scratch, size_t slot_bytes)
+{
+    using F2 = typename F2T<F>::T;
+    __shared__ int red[16 * 4];
+    __shared__ unsigned long long acc[6];
+    unsigned char *base = scratch + slot_bytes * blockIdx.x;
+    F *app = reinterpret_cast<F *>(base);
+    F2 *m12 = reinterpret_cast<F2 *>(base + layered_m12_off(fs, sizeof(F)));
+    uint32_t *meta = reinterpret_cast<uint32_t *>(m12 + ls.M_pad);
+    if (threadIdx.x == 0) {
+        app[fs.ngroups * 64] = dinf<F>();
+#pragma unroll
+        for (int q = 0; q < 6; ++q) acc[q] = 0;
+    }
+    for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
+        decode_layered_cw<F, SRC, DC, R>(a, g, fs, ls, b, app, m12, meta, red, acc);
+    flush_acc(a, acc);
+}
+
 // s += r for every codeword of a pack (one v_pk_add_f32 for two fp32 codewords).
 template <typename F, int C>
 __device__ __forceinline__ void padd(Pack<F, C> &s, const Pack<F, C> &r)
@@ -1173,7 +1445,7 @@ KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, cons
     const bool want_lds = force && force[0] == 'l';
     const bool want_global = force && force[0] == 'g';
     const bool want_flood = force && force[0] == 'f';
-    if (fs && fs->M_pad > 0 && fs->dc <= 32 && want_flood) {
+    if (fs && fs->M_pad > 0 && fs->dc <= kPackedMaxDc && want_flood) {
         kc.name = "flood";
         kc.lds_bytes = 0;
         kc.threads = 512;
@@ -1195,7 +1467,7 @@ KernelChoice choose_kernel(const DevGraph &g, bool f64, const RowSched *rs, cons
     if (lds <= kMaxLds && !want_global && !want_flood) {
         kc.name = "lds";
         kc.lds_bytes = (int)lds;
-    } else if (fs && fs->M_pad > 0 && fs->dc <= 32 && !want_global) {
+    } else if (fs && fs->M_pad > 0 && fs->dc <= kPackedMaxDc && !want_global) {
         kc.name = "flood";
         kc.lds_bytes = 0;
         kc.threads = 512;
@@ -1345,6 +1617,95 @@ int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc)
                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_decode_global<float, SRC_PHILOX>,
                                                                kc.threads, 0);
     }
+    if (e != hipSuccess) { (void)hipGetLastError(); return 0; }
+    return nb;
+}
+
+
+// ---------------------------------------------------------------- layered
+// Rows per thread per pass: the global kernel batches R rows' gathers
+// (latency of the L2/Infinity Cache), the LDS kernel does one row at a time.
+static int layered_rows_per_pass(bool global, bool f64) { return global ? (f64 ? 1 : 4) : 1; }
+
+static int layered_threads(const LayerSched &ls, int R, int cap)
+{
+    int t = ((ls.max_layer + R - 1) / R + 63) / 64 * 64;
+    return t < 64 ? 64 : (t > cap ? cap : t);
+}
+
+KernelChoice choose_layered(const DevGraph &g, bool f64, const FloodSched &fs, const LayerSched &ls, const char *force)
+{
+    (void)g;
+    KernelChoice kc;
+    kc.cw_per_block = 1;
+    kc.scratch_per_block = 0;
+    kc.lds_bytes = 0;
+    const size_t st = layered_state_bytes(fs, ls, f64 ? 8 : 4);
+    const bool want_global = force && force[0] == 'g';
+    if (st <= kMaxLds - 2048 && !want_global) {
+        kc.name = "layered_lds";
+        kc.lds_bytes = (int)st;
+        kc.threads = layered_threads(ls, layered_rows_per_pass(false, f64), 512);
+    } else {
+        kc.name = "layered_global";
+        kc.scratch_per_block = st;
+        kc.threads = layered_threads(ls, layered_rows_per_pass(true, f64), 512);
+    }
+    return kc;
+}
+
+template <typename F, int SRC, int DC>
+static hipError_t launch_layered_t(const DecodeArgs &a, const DevGraph &g, const KernelChoice &kc,
+                                   const FloodSched &fs, const LayerSched &ls, void *gs, int gblocks, hipStream_t s)
+{
+    if (kc.lds_bytes > 0) {
+        auto fn = k_decode_layered_lds<F, SRC, DC, 1>;
+        hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, kc.lds_bytes);
+        if (e != hipSuccess) return e;
+        int per_cu = 0;
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kc.threads, kc.lds_bytes);
+        if (e != hipSuccess || per_cu < 1) per_cu = 1;
+        int grid = per_cu * gblocks;   // gblocks = number of CUs here
+        if (grid > a.batch) grid = a.batch;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a, g, fs, ls);
+    } else {
+        const int grid = gblocks < a.batch ? gblocks : a.batch;
+        constexpr int R = sizeof(F) == 4 ? 4 : 1;   // layered_rows_per_pass(true, f64)
+        hipLaunchKernelGGL((k_decode_layered_global<F, SRC, DC, R>), dim3(grid), dim3(kc.threads), 0, s, a, g, fs, ls,
+                           (unsigned char *)gs, kc.scratch_per_block);
+    }
+    return hipGetLastError();
+}
+
+template <typename F, int SRC>
+static hipError_t launch_layered_dc(const DecodeArgs &a, const DevGraph &g, const KernelChoice &kc,
+                                    const FloodSched &fs, const LayerSched &ls, void *gs, int gblocks, hipStream_t s)
+{
+    if (fs.dc <= 8) return launch_layered_t<F, SRC, 8>(a, g, kc, fs, ls, gs, gblocks, s);
+    if (fs.dc <= 16) return launch_layered_t<F, SRC, 16>(a, g, kc, fs, ls, gs, gblocks, s);
+    if (fs.dc <= kPackedMaxDc) return launch_layered_t<F, SRC, kPackedMaxDc>(a, g, kc, fs, ls, gs, gblocks, s);
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_layered(const DevGraph &g, const DecodeArgs &a, bool f64, const KernelChoice &kc,
+                          const FloodSched &fs, const LayerSched &ls, void *gscratch, int gscratch_blocks,
+                          hipStream_t s)
+{
+    if (a.batch <= 0) return hipSuccess;
+    if (ls.nlayers <= 0 || !ls.lptr) return hipErrorInvalidValue;
+    if (f64)
+        return a.src == SRC_GIVEN ? launch_layered_dc<double, SRC_GIVEN>(a, g, kc, fs, ls, gscratch, gscratch_blocks, s)
+                                  : launch_layered_dc<double, SRC_PHILOX>(a, g, kc, fs, ls, gscratch, gscratch_blocks, s);
+    return a.src == SRC_GIVEN ? launch_layered_dc<float, SRC_GIVEN>(a, g, kc, fs, ls, gscratch, gscratch_blocks, s)
+                              : launch_layered_dc<float, SRC_PHILOX>(a, g, kc, fs, ls, gscratch, gscratch_blocks, s);
+}
+
+int layered_blocks_per_cu(bool f64, const KernelChoice &kc)
+{
+    int nb = 0;
+    const void *fn = f64 ? (const void *)k_decode_layered_global<double, SRC_PHILOX, 8, 1>
+                         : (const void *)k_decode_layered_global<float, SRC_PHILOX, 8, 4>;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads, 0);
     if (e != hipSuccess) { (void)hipGetLastError(); return 0; }
     return nb;
 }

@@ -21,6 +21,8 @@ if os.environ.get("LDPC_LIB"):
 LDPC_OK = 0
 MS, NMS, OMS = 0, 1, 2
 F32, F64 = 0, 1
+FLOODING, LAYERED = 0, 1
+ABI_VERSION = 2
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
@@ -48,7 +50,8 @@ FRAME_DTYPE = np.dtype([("bit_err", np.int32), ("uncoded_bit_err", np.int32),
 class _Cfg(C.Structure):
     _fields_ = [("variant", C.c_int32), ("precision", C.c_int32), ("T", C.c_int32),
                 ("quantize", C.c_int32), ("saturate", C.c_int32), ("qbits", C.c_int32),
-                ("ymax", C.c_double), ("alpha", C.c_double), ("delta", C.c_double)]
+                ("ymax", C.c_double), ("alpha", C.c_double), ("delta", C.c_double),
+                ("schedule", C.c_int32), ("reserved", C.c_int32)]
 
 
 @dataclass
@@ -63,10 +66,11 @@ class DecoderConfig:
     saturate: bool = False       # -D saturateSamples
     ymax: float = 0.0
     qbits: int = 0
+    schedule: int = FLOODING     # FLOODING (the reference's) | LAYERED (row-serial, config 3)
 
     def _c(self) -> _Cfg:
         return _Cfg(self.variant, self.precision, self.T, int(self.quantize), int(self.saturate),
-                    self.qbits, self.ymax, self.alpha, self.delta)
+                    self.qbits, self.ymax, self.alpha, self.delta, self.schedule, 0)
 
 
 _lib = None
@@ -88,6 +92,7 @@ def lib():
         "ldpc_graph_info": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),
                              C.POINTER(i32)], i32),
         "ldpc_graph_destroy": ([vp], None),
+        "ldpc_graph_layers": ([vp, vp, vp, C.POINTER(i32)], i32),
         "ldpc_device_count": ([C.POINTER(i32)], i32),
         "ldpc_ctx_create": ([i32, vp, i32, C.POINTER(vp)], i32),
         "ldpc_ctx_set_stream": ([vp, vp], i32),
@@ -108,13 +113,15 @@ def lib():
         fn = getattr(L, name)
         fn.argtypes = argt
         fn.restype = rest
+    if L.ldpc_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {L.ldpc_abi_version()}, this binding needs {ABI_VERSION}")
     _lib = L
     return L
 
 
 # Every symbol include/ldpc_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = ["ldpc_abi_version", "ldpc_last_error", "ldpc_graph_create", "ldpc_graph_load_alist",
-            "ldpc_graph_info", "ldpc_graph_destroy", "ldpc_device_count", "ldpc_ctx_create",
+            "ldpc_graph_info", "ldpc_graph_destroy", "ldpc_graph_layers", "ldpc_device_count", "ldpc_ctx_create",
             "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
             "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",
             "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info"]
@@ -157,6 +164,15 @@ class Graph:
         h = C.c_void_p()
         _check(lib().ldpc_graph_create(N, M, num_n, np_, num_m, mp_, C.byref(h)))
         return cls(h)
+
+    def layers(self):
+        """(row_order [M] int32, layer_ptr [nlayers+1] int32) of the LAYERED schedule."""
+        n = C.c_int()
+        _check(lib().ldpc_graph_layers(self._h, None, None, C.byref(n)))
+        order = np.empty(self.M, dtype=np.int32)
+        ptr = np.empty(n.value + 1, dtype=np.int32)
+        _check(lib().ldpc_graph_layers(self._h, order.ctypes.data, ptr.ctypes.data, C.byref(n)))
+        return order, ptr
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -250,6 +250,65 @@ void orc_decode_f32(const orc_alist *H, const float *yq, int T,
 }
 
 /* ===================================================================== */
+/* Layered (row-serial) normalized/offset min-sum -- SURVEY §8(f) row 2,  */
+/* BASELINE config 3. The reference has no layered schedule; this is the  */
+/* standard row-serial restatement of its check-node rule, so parity for  */
+/* layered-specific results is against this oracle only ("parity          */
+/* unpinned" w.r.t. the reference; its flooding results stay pinned).     */
+/*   app[i] = yq[i];  c2v[j][k] = 0                                        */
+/*   for each iteration, for each row j in `order` (serially):             */
+/*     x_k  = app[b_k] - c2v[j][k]                 (v2c, as :469)          */
+/*     c_k  = (k == amin ? prod*mn2 : prod*mn1) * sgn(x_k)  (:426-447)     */
+/*     c_k /= alpha (NMS, :498) | offset (OMS, :509-513)                   */
+/*     c2v[j][k] = c_k;  app[b_k] = x_k + c_k                              */
+/*   d[i] = app[i] > 0 ? +1 : -1                    (:471-474)             */
+/* Rows that share no bit commute exactly, so any grouping of consecutive  */
+/* bit-disjoint rows of `order` into parallel layers gives these results.  */
+/* ===================================================================== */
+#define ORC_DEFINE_LAYERED(FT, SUFFIX, SGN, FABS)                                  \
+void orc_decode_layered_##SUFFIX(const orc_alist *H, const FT *yq, int T,         \
+                                 const orc_cfg *cfg, const int32_t *order,        \
+                                 int8_t *d)                                       \
+{                                                                                 \
+    const int N = H->N, M = H->M, dc = H->maxdc > 0 ? H->maxdc : 1;               \
+    const FT alpha = (FT)cfg->alpha, delta = (FT)cfg->delta;                      \
+    FT *app = (FT *)malloc(sizeof(FT) * (N + 1));                                 \
+    FT *c2v = (FT *)calloc((size_t)M * dc + 1, sizeof(FT));                       \
+    FT *x = (FT *)malloc(sizeof(FT) * (dc + 1));                                  \
+    for (int i = 0; i < N; ++i) app[i] = yq[i];                                   \
+    for (int it = 0; it < T; ++it) {                                              \
+        for (int r = 0; r < M; ++r) {                                             \
+            const int j = order ? order[r] : r;                                   \
+            const int *row = H->mlist + (long)j * H->maxdc;                       \
+            FT *cj = c2v + (long)j * dc;                                          \
+            FT mn1 = (FT)INFINITY, mn2 = (FT)INFINITY, prod = 1;                  \
+            int amin = -1;                                                        \
+            for (int k = 0; k < H->deg_m[j]; ++k) {                               \
+                x[k] = app[row[k] - 1] - cj[k];                                   \
+                prod *= SGN(x[k]);                                                \
+                if (FABS(x[k]) <= mn1) { mn2 = mn1; mn1 = FABS(x[k]); amin = k; } \
+                else if (FABS(x[k]) < mn2) mn2 = FABS(x[k]);                      \
+            }                                                                     \
+            for (int k = 0; k < H->deg_m[j]; ++k) {                               \
+                FT c = (k == amin ? prod * mn2 : prod * mn1) * SGN(x[k]);         \
+                if (cfg->variant == ORC_NMS) c /= alpha;                          \
+                else if (cfg->variant == ORC_OMS) {                               \
+                    FT mag = FABS(c) - delta;                                     \
+                    c = mag > 0 ? SGN(c) * mag : 0;                               \
+                }                                                                 \
+                cj[k] = c;                                                        \
+                app[row[k] - 1] = x[k] + c;                                       \
+            }                                                                     \
+        }                                                                         \
+    }                                                                             \
+    for (int i = 0; i < N; ++i) d[i] = app[i] > 0 ? 1 : -1;                       \
+    free(app); free(c2v); free(x);                                                \
+}
+
+ORC_DEFINE_LAYERED(double, f64, sgn_d, fabs)
+ORC_DEFINE_LAYERED(float, f32, sgn_f, fabsf)
+
+/* ===================================================================== */
 /* The Monte-Carlo frame loop of main() (decodeMinSum.cpp:146-311).      */
 /* ===================================================================== */
 int64_t orc_minsum_run(const orc_alist *H, double R, double snr, int T,

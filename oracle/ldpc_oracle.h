@@ -98,6 +98,14 @@ void orc_decode_f64_snap(const orc_alist *H, const double *yq, int T,
                          const orc_cfg *cfg, int8_t *d,
                          int snap_it, double *c2v_out, double *app_out);
 
+/* Layered (row-serial) min-sum in the row order `order` [M] (NULL = 0..M-1);
+ * same check-node rule, normalisation and offset as above, app updated in
+ * place (see ldpc_oracle.c). No reference counterpart: own restatement. */
+void orc_decode_layered_f64(const orc_alist *H, const double *yq, int T,
+                            const orc_cfg *cfg, const int32_t *order, int8_t *d);
+void orc_decode_layered_f32(const orc_alist *H, const float *yq, int T,
+                            const orc_cfg *cfg, const int32_t *order, int8_t *d);
+
 /* Philox4x32-10 (Random123 reference constants). */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 

@@ -71,6 +71,9 @@ def lib():
                                          C.POINTER(_Cfg), C.c_void_p]
         L.orc_decode_f64_snap.argtypes = [C.POINTER(_Alist), C.c_void_p, C.c_int, C.POINTER(_Cfg),
                                           C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        for name in ("orc_decode_layered_f64", "orc_decode_layered_f32"):
+            getattr(L, name).argtypes = [C.POINTER(_Alist), C.c_void_p, C.c_int,
+                                         C.POINTER(_Cfg), C.c_void_p, C.c_void_p]
         L.orc_philox4x32_10.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         _LIB = L
     return _LIB
@@ -151,6 +154,22 @@ class Alist:
         cc = cfg.c()
         for b in range(yq2.shape[0]):
             fn(C.byref(self._a), yq2[b].ctypes.data, T, C.byref(cc), d[b].ctypes.data)
+        return d[0] if single else d
+
+    def decode_layered(self, yq: np.ndarray, T: int, cfg: Cfg, order=None) -> np.ndarray:
+        """Layered (row-serial) decode of a [B, N] or [N] batch in row order `order`."""
+        yq = np.ascontiguousarray(yq)
+        single = yq.ndim == 1
+        yq2 = yq.reshape(-1, self.N)
+        d = np.empty(yq2.shape, dtype=np.int8)
+        assert yq2.dtype in (np.float64, np.float32)
+        fn = lib().orc_decode_layered_f64 if yq2.dtype == np.float64 else lib().orc_decode_layered_f32
+        o = None if order is None else np.ascontiguousarray(order, dtype=np.int32)
+        assert o is None or o.shape == (self.M,)
+        cc = cfg.c()
+        for b in range(yq2.shape[0]):
+            fn(C.byref(self._a), yq2[b].ctypes.data, T, C.byref(cc),
+               None if o is None else o.ctypes.data, d[b].ctypes.data)
         return d[0] if single else d
 
     def decode_snap(self, yq: np.ndarray, T: int, cfg: Cfg, snap_it: int):

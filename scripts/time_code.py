@@ -2,6 +2,7 @@
 """Time the fused on-device simulation for one code: decoded Mbit/s and the kernel chosen.
 
 usage: time_code.py ALIST [--batch B] [--T T] [--snr DB] [--variant ms|nms|oms] [--prec f32|f64] [--reps R]
+                    [--schedule flooding|layered]
 """
 import argparse
 import os
@@ -22,12 +23,14 @@ def main():
     ap.add_argument("--variant", default="nms")
     ap.add_argument("--prec", default="f32")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--schedule", choices=["flooding", "layered"], default="flooding")
     a = ap.parse_args()
     g = native.Graph.from_alist(a.alist)
     ctx = native.Context(g, 0, a.batch)
     v = {"ms": dict(variant=native.MS), "nms": dict(variant=native.NMS, alpha=1.25),
          "oms": dict(variant=native.OMS, delta=0.15)}[a.variant]
-    cfg = native.DecoderConfig(T=a.T, precision=native.F32 if a.prec == "f32" else native.F64, **v)
+    cfg = native.DecoderConfig(T=a.T, precision=native.F32 if a.prec == "f32" else native.F64,
+                               schedule=native.LAYERED if a.schedule == "layered" else native.FLOODING, **v)
     info = ctx.kernel_info(cfg)
     ctx.sim_batch(a.snr, a.rate, cfg, seed=1, stream_id=0, first_cw=0, batch=a.batch)   # warm-up
     best = 1e30
@@ -38,7 +41,7 @@ def main():
         best = min(best, dt)
     mbit = g.N * a.batch / best / 1e6
     print(f"{os.path.basename(a.alist)} N={g.N} batch={a.batch} T={a.T} {a.variant}/{a.prec}: "
-          f"{best*1e3:.1f} ms/batch  {mbit:.1f} Mbit/s  kernel={info}  last FER={cnt.frame_err}/{cnt.frames}")
+          f"{a.schedule} {best*1e3:.1f} ms/batch  {mbit:.1f} Mbit/s  kernel={info}  last FER={cnt.frame_err}/{cnt.frames}")
 
 
 if __name__ == "__main__":
