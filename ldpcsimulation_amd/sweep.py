@@ -11,6 +11,9 @@ line for each point.
     python -m ldpcsimulation_amd.sweep ALIST --rate 0.5 --snr 1.0 1.25 1.5 -T 50 \\
         --variant nms --alpha 1.25 --log results.txt
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m ldpcsimulation_amd.sweep ...
+    # BASELINE config 3: DVB-S2 N=64800 R1/2, layered NMS, SNR sweep over 8 GPUs
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m ldpcsimulation_amd.sweep dvbs2_1_2.alist \\
+        --rate 0.5 --snr 0.8 0.9 1.0 1.1 -T 50 --variant nms --alpha 1.25 --schedule layered --batch 2048
 """
 from __future__ import annotations
 
@@ -37,6 +40,8 @@ def parse(argv=None):
     p.add_argument("--quantize", nargs=2, metavar=("YMAX", "Q"), help="-D quantizeSamples front-end")
     p.add_argument("--saturate", type=float, metavar="YMAX", help="-D saturateSamples front-end")
     p.add_argument("--precision", choices=["f32", "f64"], default="f32")
+    p.add_argument("--schedule", choices=["flooding", "layered"], default="flooding",
+                   help="flooding = the reference's schedule; layered = row-serial (BASELINE config 3)")
     p.add_argument("--batch", type=int, default=65536, help="frames per GPU per round")
     p.add_argument("--seed", type=int, default=None, help="noise seed (default: time)")
     p.add_argument("--min-bit-errors", type=int, default=200)
@@ -61,7 +66,8 @@ def main(argv=None) -> int:
         dist.init_process_group("nccl", device_id=torch.device("cuda", device))
     seed = a.seed if a.seed is not None else int(time.time())
     cfg = native.DecoderConfig(variant=VARIANTS[a.variant], T=a.iterations, alpha=a.alpha, delta=a.delta,
-                               precision=native.F64 if a.precision == "f64" else native.F32)
+                               precision=native.F64 if a.precision == "f64" else native.F32,
+                               schedule=native.LAYERED if a.schedule == "layered" else native.FLOODING)
     extra = []
     if a.quantize:
         cfg.quantize, cfg.ymax, cfg.qbits = True, float(a.quantize[0]), int(a.quantize[1])

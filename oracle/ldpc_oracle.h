@@ -106,6 +106,36 @@ void orc_decode_layered_f64(const orc_alist *H, const double *yq, int T,
 void orc_decode_layered_f32(const orc_alist *H, const float *yq, int T,
                             const orc_cfg *cfg, const int32_t *order, int8_t *d);
 
+/* ---- GDBF / NGDBF bit flipping (src/decodeGDBF.cpp, parallel mode) ---- */
+enum {
+    ORC_GDBF_NOISE = 1,      /* -D addNoise            */
+    ORC_GDBF_ADAPT = 2,      /* -D thresholdAdaptation */
+    ORC_GDBF_WEIGHT = 4,     /* -D weightSyndromes     */
+    ORC_GDBF_SMOOTH = 8,     /* -D outputSmoothing     */
+    ORC_GDBF_SATURATE = 16,  /* -D saturateSamples     */
+    ORC_GDBF_QUANTIZE = 32   /* -D quantizeSamples     */
+};
+typedef struct {
+    int    flags, T, windowsize, nq;
+    double theta, lambda, alpha, noise_scale, ymax;
+} orc_gdbf_cfg;
+/* channel front-end of one sample (:254-267): returns yq, *r = hard decision */
+double orc_gdbf_front(double y, const orc_gdbf_cfg *cfg, int *r);
+float  orc_gdbf_front_f32(float y, const orc_gdbf_cfg *cfg, int *r);
+/* One frame (:298-367): d = r on entry, decisions on exit; pert [T][N]
+ * (iteration it uses row it; NULL without ORC_GDBF_NOISE). Returns the
+ * iterations run; *satisfied = all checks satisfied (early stop). */
+int orc_gdbf_decode_f64(const orc_alist *H, const double *yq, const double *pert,
+                        const orc_gdbf_cfg *cfg, int8_t *d, int *satisfied);
+int orc_gdbf_decode_f32(const orc_alist *H, const float *yq, const float *pert,
+                        const orc_gdbf_cfg *cfg, int8_t *d, int *satisfied);
+/* main() frame loop (:224-413): stop rule errors >= 200 && wordErrors >=
+ * 20/10/5 (N > 10000 / 50000) unless max_frames >= 0. */
+int64_t orc_gdbf_run(const orc_alist *H, double R, double snr, const orc_gdbf_cfg *cfg, uint32_t seed,
+                     const char *const *cw_lines, int ncw, int64_t max_frames,
+                     int32_t *frame_w, int32_t *frame_it, int64_t cap, orc_stats *out,
+                     int64_t *smoothing_used);
+
 /* Philox4x32-10 (Random123 reference constants). */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 

@@ -36,6 +36,12 @@ class _Cfg(C.Structure):
                 ("qbits", C.c_int)]
 
 
+class _GdbfCfg(C.Structure):
+    _fields_ = [("flags", C.c_int), ("T", C.c_int), ("windowsize", C.c_int), ("nq", C.c_int),
+                ("theta", C.c_double), ("lambda_", C.c_double), ("alpha", C.c_double),
+                ("noise_scale", C.c_double), ("ymax", C.c_double)]
+
+
 class _Stats(C.Structure):
     _fields_ = [("errors", C.c_int64), ("uncoded", C.c_int64), ("bits", C.c_int64),
                 ("words", C.c_int64), ("word_errors", C.c_int64), ("iters", C.c_int64)]
@@ -75,6 +81,18 @@ def lib():
             getattr(L, name).argtypes = [C.POINTER(_Alist), C.c_void_p, C.c_int,
                                          C.POINTER(_Cfg), C.c_void_p, C.c_void_p]
         L.orc_philox4x32_10.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_gdbf_front.argtypes = [C.c_double, C.POINTER(_GdbfCfg), C.POINTER(C.c_int)]
+        L.orc_gdbf_front.restype = C.c_double
+        L.orc_gdbf_front_f32.argtypes = [C.c_float, C.POINTER(_GdbfCfg), C.POINTER(C.c_int)]
+        L.orc_gdbf_front_f32.restype = C.c_float
+        for name in ("orc_gdbf_decode_f64", "orc_gdbf_decode_f32"):
+            getattr(L, name).argtypes = [C.POINTER(_Alist), C.c_void_p, C.c_void_p, C.POINTER(_GdbfCfg),
+                                         C.c_void_p, C.POINTER(C.c_int)]
+            getattr(L, name).restype = C.c_int
+        L.orc_gdbf_run.argtypes = [C.POINTER(_Alist), C.c_double, C.c_double, C.POINTER(_GdbfCfg), C.c_uint32,
+                                   C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
+                                   C.POINTER(_Stats), C.POINTER(C.c_int64)]
+        L.orc_gdbf_run.restype = C.c_int64
         _LIB = L
     return _LIB
 
@@ -115,6 +133,27 @@ class Cfg:
     def c(self) -> _Cfg:
         return _Cfg(self.variant, self.alpha, self.delta, int(self.quantize),
                     int(self.saturate), self.ymax, self.qbits)
+
+
+GDBF_NOISE, GDBF_ADAPT, GDBF_WEIGHT, GDBF_SMOOTH, GDBF_SATURATE, GDBF_QUANTIZE = 1, 2, 4, 8, 16, 32
+
+
+@dataclass
+class GdbfCfg:
+    """decodeGDBF.cpp parallel mode; flags = the -D switches (GDBF_*)."""
+    flags: int = 0
+    T: int = 100
+    theta: float = -0.9
+    lambda_: float = 1.0
+    alpha: float = 1.0
+    noise_scale: float = 0.0
+    ymax: float = 0.0
+    windowsize: int = 64
+    nq: int = 16
+
+    def c(self) -> _GdbfCfg:
+        return _GdbfCfg(self.flags, self.T, self.windowsize, self.nq, self.theta, self.lambda_, self.alpha,
+                        self.noise_scale, self.ymax)
 
 
 class Alist:
@@ -171,6 +210,42 @@ class Alist:
             fn(C.byref(self._a), yq2[b].ctypes.data, T, C.byref(cc),
                None if o is None else o.ctypes.data, d[b].ctypes.data)
         return d[0] if single else d
+
+    def gdbf_decode(self, y: np.ndarray, pert, cfg: GdbfCfg):
+        """One GDBF/NGDBF frame from RAW channel samples y [N] (front-end applied here)
+        and perturbations pert [T][N] (or None). Returns (d, iterations, satisfied)."""
+        f32 = y.dtype == np.float32
+        front = lib().orc_gdbf_front_f32 if f32 else lib().orc_gdbf_front
+        cc = cfg.c()
+        r = C.c_int()
+        yq = np.empty(self.N, dtype=y.dtype)
+        d = np.empty(self.N, dtype=np.int8)
+        for i in range(self.N):
+            yq[i] = front(float(y[i]), C.byref(cc), C.byref(r))
+            d[i] = r.value
+        p = None if pert is None else np.ascontiguousarray(pert, dtype=y.dtype)
+        sat = C.c_int()
+        fn = lib().orc_gdbf_decode_f32 if f32 else lib().orc_gdbf_decode_f64
+        it = fn(C.byref(self._a), yq.ctypes.data, None if p is None else p.ctypes.data, C.byref(cc),
+                d.ctypes.data, C.byref(sat))
+        return d, it, bool(sat.value)
+
+    def gdbf_run(self, R, snr, cfg: GdbfCfg, seed, cw_lines=None, max_frames=-1, cap=0):
+        st = _Stats()
+        su = C.c_int64()
+        fw = np.zeros(max(cap, 1), dtype=np.int32)
+        fi = np.zeros(max(cap, 1), dtype=np.int32)
+        if cw_lines:
+            arr = (C.c_char_p * len(cw_lines))(*[s.encode() for s in cw_lines])
+            cwp, ncw = C.cast(arr, C.c_void_p), len(cw_lines)
+        else:
+            arr, cwp, ncw = None, None, 0
+        n = lib().orc_gdbf_run(C.byref(self._a), R, snr, C.byref(cfg.c()), seed & 0xFFFFFFFF, cwp, ncw,
+                               max_frames, fw.ctypes.data if cap else None, fi.ctypes.data if cap else None,
+                               cap, C.byref(st), C.byref(su))
+        k = min(n, cap)
+        return n, {**{k2: getattr(st, k2) for k2, _ in _Stats._fields_}, "smoothing_used": su.value}, \
+            fw[:k], fi[:k]
 
     def decode_snap(self, yq: np.ndarray, T: int, cfg: Cfg, snap_it: int):
         yq = np.ascontiguousarray(yq, dtype=np.float64)

@@ -33,9 +33,12 @@ def code_path(name: str) -> str:
     return p
 
 
-def golden_runs():
+def golden_runs(kind: str = "minsum"):
+    """Reference runs of tests/golden/reference_runs.json: kind "minsum" (decodeMinSum
+    family) or "gdbf" (decodeGDBF family)."""
     with open(os.path.join(GOLD, "reference_runs.json")) as f:
-        return json.load(f)["runs"]
+        runs = json.load(f)["runs"]
+    return [r for r in runs if ("GDBF" in r["binary"]) == (kind == "gdbf")]
 
 
 @pytest.fixture(scope="session")

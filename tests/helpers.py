@@ -29,3 +29,43 @@ def cw_lines(run):
 def final_numbers(final_line):
     m = re.match(r"Final result: (\d+) bit errs in (\d+) words.*Uncoded errors = (\d+)", final_line)
     return tuple(int(x) for x in m.groups())
+
+
+# decodeGDBF.cpp Makefile targets (C_implementations/Makefile:33-53) -> -D switches
+GDBF_BINARIES = {
+    "decodeMNGDBF": ("noise", "adapt", "weight", "saturate"),
+    "decodeSMNGDBF": ("noise", "adapt", "weight", "smooth", "saturate"),
+    "decodeATGDBF": ("adapt",),
+    "decodeSATGDBF": ("adapt", "smooth"),
+    "decodeSMGDBF": ("smooth",),
+}
+
+
+def gdbf_config(run):
+    """(R, snr, dict of oracle GdbfCfg fields) of a golden GDBF reference run. Positional
+    arguments after the log file follow decodeGDBF.cpp:95-113: noiseScale, [NQ], lambda,
+    alpha, windowsize, Ymax -- each present only with its switch."""
+    from oracle import oracle as O
+    a = run["args"]
+    R, snr, T, theta = float(a[0]), float(a[1]), int(a[2]), float(a[3])
+    rest = a[5:]
+    sw = GDBF_BINARIES[run["binary"]]
+    bits = {"noise": O.GDBF_NOISE, "adapt": O.GDBF_ADAPT, "weight": O.GDBF_WEIGHT,
+            "smooth": O.GDBF_SMOOTH, "saturate": O.GDBF_SATURATE}
+    cfg = dict(flags=sum(bits[s] for s in sw), T=T, theta=theta, lambda_=0.991, alpha=2.25,
+               noise_scale=1.0, ymax=2.25, windowsize=64)   # the reference's defaults (:48-56)
+    i = 0
+    for name, key, conv in (("noise", "noise_scale", float), ("adapt", "lambda_", float),
+                            ("weight", "alpha", float), ("smooth", "windowsize", int),
+                            ("saturate", "ymax", float)):
+        if name in sw:
+            cfg[key] = conv(rest[i])
+            i += 1
+    return R, snr, cfg
+
+
+def gdbf_final_numbers(final_line):
+    """(bit errors, words, average iterations, uncoded errors) of a GDBF 'Final result' line."""
+    m = re.match(r"Final result: (\d+) bit errs in (\d+) words.*Average iterations = ([0-9.e+-]+)\. "
+                 r"Uncoded errors = (\d+)", final_line)
+    return int(m.group(1)), int(m.group(2)), float(m.group(3)), int(m.group(4))
