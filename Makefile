@@ -12,7 +12,7 @@ HIPFLAGS  = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iincl
 CXXFLAGS  = -O2 -std=c++17 -ffp-contract=off -Iinclude -Wall
 
 LIB       = $(LIBDIR)/libldpc_hip.so
-OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
+OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
 CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalizedMinSum $(BINDIR)/decodeOffsetMinSum
 
 all: $(LIB) $(CLIS) oracle
@@ -25,9 +25,11 @@ $(BINDIR):
 # -load-store-opt: keep the bit-phase LDS reads as single ds_read_b64 (2 LDS
 # cycles each) instead of merged ds_read2st64_b64 (8 cycles for the same data).
 KERNFLAGS = -Xclang -target-feature -Xclang -load-store-opt
-$(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h | $(LIBDIR)/obj
+$(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
-$(LIBDIR)/obj/api.o: $(CSRC)/api.cpp $(CSRC)/kernels.h $(CSRC)/graph.h include/ldpc_hip.h | $(LIBDIR)/obj
+$(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+$(LIBDIR)/obj/api.o: $(CSRC)/api.cpp $(CSRC)/kernels.h $(CSRC)/gdbf.h $(CSRC)/graph.h include/ldpc_hip.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/graph.o: $(CSRC)/graph.cpp $(CSRC)/graph.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -54,7 +56,7 @@ variant:
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/api.o $(CSRC)/api.cpp
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/graph.o
+	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/graph.o
 
 oracle:
 	$(MAKE) -f oracle/Makefile

@@ -23,6 +23,10 @@
  *   The compile-time variants of the reference (-D normalizedMS, offsetMS,
  *   quantizeSamples, saturateSamples; src/decodeMinSum.cpp:26-32,
  *   Makefile:58-65) are runtime fields of ldpc_decoder_cfg.
+ *   - ldpc_gdbf_decode_batch / ldpc_gdbf_sim_* replace the frame body of the
+ *     GDBF / NGDBF bit-flipping decoders (src/decodeGDBF.cpp:250-399,
+ *     checkNodeUpdates :517-534, symNodeUpdates :536-621), whose -D switches
+ *     (Makefile:33-53) are the flags of ldpc_gdbf_cfg.
  *
  * Conventions: every function returns LDPC_OK (0) or a negative
  * ldpc_status; ldpc_last_error() gives a thread-local message. No C++
@@ -41,7 +45,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 2
+#define LDPC_ABI_VERSION 3
 
 typedef enum {
     LDPC_OK = 0,
@@ -88,7 +92,7 @@ typedef struct {
     int32_t bit_err;          /* newErrors of :270 (0 = frame decoded)  */
     int32_t uncoded_bit_err;  /* hard-decision errors before decoding    */
     int32_t syndrome_fail;    /* 1 if H*d != 0                          */
-    int32_t reserved;
+    int32_t iters;            /* GDBF: iterations run (`it`, decodeGDBF.cpp:399); min-sum: 0 */
 } ldpc_frame_result;
 
 typedef struct {
@@ -190,6 +194,59 @@ int  ldpc_ctx_last_kernel_ms(ldpc_ctx *ctx, float *ms);
  * forces the global-memory kernel, for testing it on small codes. */
 int  ldpc_ctx_kernel_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, char *name, int name_len,
                           int *lds_bytes, int *blocks_per_cu);
+
+/* ---- GDBF / NGDBF bit flipping (BASELINE config 4) --------------------- */
+/* src/decodeGDBF.cpp in its parallel-flip mode (mu = 1): syndrome check
+ * nodes with early stop (:298-306, :517-534), energy E = d*yq + w*sum(s)
+ * [+ perturbation] and flip when E < theta (:536-621). The compile-time
+ * switches of C_implementations/Makefile:33-53 are runtime flags:
+ * decodeMNGDBF = NOISE|ADAPT|WEIGHT|SATURATE, decodeSMNGDBF = the same|SMOOTH,
+ * decodeATGDBF = ADAPT, decodeSATGDBF = ADAPT|SMOOTH, decodeSMGDBF = SMOOTH.
+ * (modeswitching / sequentialmode / quantizeProbabilities: not supported.) */
+typedef enum {
+    LDPC_GDBF_NOISE = 1,      /* -D addNoise: E += noiseScale*sigma*n per bit and iteration */
+    LDPC_GDBF_ADAPT = 2,      /* -D thresholdAdaptation: theta *= lambda when not flipped   */
+    LDPC_GDBF_WEIGHT = 4,     /* -D weightSyndromes: syndrome weight alpha (else 1)         */
+    LDPC_GDBF_SMOOTH = 8,     /* -D outputSmoothing: majority of the last windowsize d's    */
+    LDPC_GDBF_SATURATE = 16,  /* -D saturateSamples: |yq| <= Ymax                           */
+    LDPC_GDBF_QUANTIZE = 32   /* -D quantizeSamples: quantize(yq) with NQ levels            */
+} ldpc_gdbf_flag;
+
+typedef struct {
+    int32_t flags;        /* OR of ldpc_gdbf_flag                         */
+    int32_t precision;    /* ldpc_precision                               */
+    int32_t T;            /* num_iterations (maximum; early stop)         */
+    int32_t windowsize;   /* outputSmoothing window                       */
+    int32_t nq;           /* quantizeSamples NQ                           */
+    int32_t reserved;     /* 0                                            */
+    double  theta;        /* initial flip threshold                       */
+    double  lambda;       /* threshold adaptation factor                  */
+    double  alpha;        /* syndrome weight (weightSyndromes)            */
+    double  noise_scale;  /* perturbation sigma = noise_scale * channel sigma */
+    double  ymax;         /* saturation / quantizer range                 */
+} ldpc_gdbf_cfg;
+
+/* Decode `batch` frames of given RAW channel samples y[batch][N] (float for
+ * F32, double for F64; host or device): front-end (:254-267), then the
+ * iterations with the caller's perturbations pert[batch][T][N] (iteration it
+ * of frame b adds pert[b][it][i] to E_i; required with LDPC_GDBF_NOISE, else
+ * ignored). c, d_out, frames, counts as ldpc_decode_batch; frames[].iters and
+ * counts->iters report the iterations run. Synchronous. Replaces the frame
+ * body of decodeGDBF.cpp main() (:250-399). */
+int  ldpc_gdbf_decode_batch(ldpc_ctx *ctx, const void *y, const void *pert, int batch, const ldpc_gdbf_cfg *cfg,
+                            const int8_t *c, int8_t *d_out, ldpc_frame_result *frames, ldpc_counts *counts);
+/* Fused on-device Monte-Carlo of one SNR point (as ldpc_sim_launch: the
+ * channel of frame f is the same as the min-sum path's); perturbations from
+ * Philox4x32-10 keyed by (seed; bit/4, frame, stream_id | (it+1) << 20).
+ * stream_id < 2^20. Asynchronous; counts accumulate in the context. */
+int  ldpc_gdbf_sim_launch(ldpc_ctx *ctx, double ebn0_db, double R, const ldpc_gdbf_cfg *cfg, uint64_t seed,
+                          uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames_dev);
+/* ldpc_gdbf_sim_launch + counts accumulated into *accum; frames host or device. Synchronous. */
+int  ldpc_gdbf_sim_batch(ldpc_ctx *ctx, double ebn0_db, double R, const ldpc_gdbf_cfg *cfg, uint64_t seed,
+                         uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames,
+                         ldpc_counts *accum);
+/* Kernel chosen for a GDBF cfg ("gdbf_lds" / "gdbf_global") and its LDS bytes. */
+int  ldpc_gdbf_kernel_info(ldpc_ctx *ctx, const ldpc_gdbf_cfg *cfg, char *name, int name_len, int *lds_bytes);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,7 @@
 // exception crosses the ABI; every HIP failure becomes LDPC_ERR_DEVICE with
 // a message in ldpc_last_error().
 #include "ldpc_hip.h"
+#include "gdbf.h"
 
 #include <hip/hip_runtime.h>
 
@@ -72,7 +73,7 @@ struct ldpc_ctx {
     int num_cus = 0;
     hipStream_t own = nullptr, stream = nullptr;
     ldpc::DevGraph dg{};
-    DevBuf graph, counts, hist, y_stage, c_stage, d_stage, fw_stage, cw_table, gscratch;
+    DevBuf graph, counts, hist, y_stage, c_stage, d_stage, fw_stage, cw_table, gscratch, p_stage;
     int cw_rows = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
@@ -195,7 +196,7 @@ static void ctx_free(ldpc_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->graph, &c->counts, &c->hist, &c->y_stage, &c->c_stage, &c->d_stage, &c->fw_stage,
-                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck, &c->fsched, &c->lsched})
+                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck, &c->fsched, &c->lsched, &c->p_stage})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -804,6 +805,209 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
     if (bpc) *bpc = is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
                                    : ldpc::blocks_per_cu(c->dg, f64, kc);
+    return LDPC_OK;
+}
+
+
+// ----------------------------------------------------------------- GDBF / NGDBF
+static int gdbf_check_cfg(const ldpc_gdbf_cfg *cfg)
+{
+    if (!cfg) return set_err(LDPC_ERR_INVALID, "cfg is null");
+    if (cfg->precision != LDPC_F32 && cfg->precision != LDPC_F64)
+        return set_err(LDPC_ERR_INVALID, "bad precision %d", cfg->precision);
+    if (cfg->T < 0 || cfg->T > 4094) return set_err(LDPC_ERR_INVALID, "T must be in 0..4094");
+    if (cfg->flags & ~63) return set_err(LDPC_ERR_INVALID, "unknown GDBF flags 0x%x", cfg->flags);
+    if ((cfg->flags & (LDPC_GDBF_SATURATE | LDPC_GDBF_QUANTIZE)) && !(cfg->ymax > 0))
+        return set_err(LDPC_ERR_INVALID, "saturate/quantize need ymax > 0");
+    if ((cfg->flags & LDPC_GDBF_QUANTIZE) && (cfg->nq < 1 || cfg->nq > 30))
+        return set_err(LDPC_ERR_INVALID, "nq out of range");
+    if ((cfg->flags & LDPC_GDBF_SMOOTH) && (cfg->windowsize < 0 || cfg->windowsize > 32767))
+        return set_err(LDPC_ERR_INVALID, "windowsize out of range");
+    return LDPC_OK;
+}
+
+static void gdbf_fill(ldpc::GdbfArgs &a, ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, int batch)
+{
+    std::memset(&a, 0, sizeof a);
+    a.batch = batch;
+    a.T = cfg->T;
+    a.flags = cfg->flags;
+    a.windowsize = cfg->windowsize;
+    a.theta0 = cfg->theta;
+    a.lambda = cfg->lambda;
+    a.w = (cfg->flags & LDPC_GDBF_WEIGHT) ? cfg->alpha : 1.0;   // :541-551
+    a.ymax = cfg->ymax;
+    a.qmax = std::pow(2, (cfg->nq - 1));                       // :490
+    a.counts = (unsigned long long *)c->counts.p;
+    a.hist = (unsigned long long *)c->hist.p;
+}
+
+static int gdbf_run(ldpc_ctx *c, const ldpc::GdbfArgs &a, bool f64)
+{
+    const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, f64);
+    int slots = 0;
+    if (ch.slot_bytes) {
+        slots = std::min(a.batch, 2 * c->num_cus);
+        HIP_TRY(c->gscratch.ensure(ch.slot_bytes * (size_t)slots));
+    }
+    HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    HIP_TRY(ldpc::gdbf_launch(c->dg, a, f64, ch, c->gscratch.p, slots, c->stream));
+    HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return LDPC_OK;
+}
+
+static int counts_delta(ldpc_ctx *c, const ldpc_counts &before, ldpc_counts *acc)
+{
+    ldpc_counts after;
+    int rc = read_counts(c, &after, 0);
+    if (rc) return rc;
+    if (acc) {
+        ldpc_counts d;
+        d.bit_err = after.bit_err - before.bit_err;
+        d.frame_err = after.frame_err - before.frame_err;
+        d.uncoded_bit_err = after.uncoded_bit_err - before.uncoded_bit_err;
+        d.frames = after.frames - before.frames;
+        d.iters = after.iters - before.iters;
+        d.syndrome_fail = after.syndrome_fail - before.syndrome_fail;
+        accumulate(acc, d);
+    }
+    return LDPC_OK;
+}
+
+int ldpc_gdbf_decode_batch(ldpc_ctx *c, const void *y, const void *pert, int batch, const ldpc_gdbf_cfg *cfg,
+                           const int8_t *cw, int8_t *d_out, ldpc_frame_result *frames, ldpc_counts *counts)
+{
+    if (!c || !y) return set_err(LDPC_ERR_INVALID, "null argument");
+    int rc = gdbf_check_cfg(cfg);
+    if (rc) return rc;
+    if (batch <= 0 || batch > c->max_batch)
+        return set_err(LDPC_ERR_INVALID, "batch %d outside 1..max_batch=%d", batch, c->max_batch);
+    if ((cfg->flags & LDPC_GDBF_NOISE) && !pert) return set_err(LDPC_ERR_INVALID, "NOISE needs pert");
+    HIP_TRY(hipSetDevice(c->device));
+    const bool f64 = cfg->precision == LDPC_F64;
+    const int N = c->g->N;
+    const size_t fsz = f64 ? 8 : 4, nb = (size_t)batch * N;
+    ldpc::GdbfArgs a;
+    gdbf_fill(a, c, cfg, batch);
+    a.src = ldpc::SRC_GIVEN;
+    if (is_device_ptr(y)) {
+        a.y = y;
+    } else {
+        HIP_TRY(c->y_stage.ensure(nb * fsz));
+        HIP_TRY(hipMemcpyAsync(c->y_stage.p, y, nb * fsz, hipMemcpyHostToDevice, c->stream));
+        a.y = c->y_stage.p;
+    }
+    if (cfg->flags & LDPC_GDBF_NOISE) {
+        const size_t pb = nb * (size_t)cfg->T * fsz;
+        if (is_device_ptr(pert)) {
+            a.pert = pert;
+        } else {
+            HIP_TRY(c->p_stage.ensure(pb));
+            HIP_TRY(hipMemcpyAsync(c->p_stage.p, pert, pb, hipMemcpyHostToDevice, c->stream));
+            a.pert = c->p_stage.p;
+        }
+    }
+    if (cw) {
+        if (is_device_ptr(cw)) {
+            a.c = cw;
+        } else {
+            HIP_TRY(c->c_stage.ensure(nb));
+            HIP_TRY(hipMemcpyAsync(c->c_stage.p, cw, nb, hipMemcpyHostToDevice, c->stream));
+            a.c = (const int8_t *)c->c_stage.p;
+        }
+    }
+    const bool d_host = d_out && !is_device_ptr(d_out);
+    const bool w_host = frames && !is_device_ptr(frames);
+    if (d_host) {
+        HIP_TRY(c->d_stage.ensure(nb));
+        a.d_out = (int8_t *)c->d_stage.p;
+    } else {
+        a.d_out = d_out;
+    }
+    if (w_host) {
+        HIP_TRY(c->fw_stage.ensure(sizeof(ldpc_frame_result) * (size_t)batch));
+        a.frame_res = (int4 *)c->fw_stage.p;
+    } else {
+        a.frame_res = (int4 *)frames;
+    }
+    ldpc_counts before;
+    rc = read_counts(c, &before, 0);
+    if (rc) return rc;
+    rc = gdbf_run(c, a, f64);
+    if (rc) return rc;
+    if (d_host) HIP_TRY(hipMemcpyAsync(d_out, c->d_stage.p, nb, hipMemcpyDeviceToHost, c->stream));
+    if (w_host)
+        HIP_TRY(hipMemcpyAsync(frames, c->fw_stage.p, sizeof(ldpc_frame_result) * (size_t)batch,
+                               hipMemcpyDeviceToHost, c->stream));
+    return counts_delta(c, before, counts);
+}
+
+static int gdbf_sim_impl(ldpc_ctx *c, double ebn0_db, double R, const ldpc_gdbf_cfg *cfg, uint64_t seed,
+                         uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames_dev)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    int rc = gdbf_check_cfg(cfg);
+    if (rc) return rc;
+    if (batch <= 0 || batch > c->max_batch)
+        return set_err(LDPC_ERR_INVALID, "batch %d outside 1..max_batch=%d", batch, c->max_batch);
+    if (!(R > 0)) return set_err(LDPC_ERR_INVALID, "rate must be > 0");
+    if (stream_id >= (1u << 20)) return set_err(LDPC_ERR_INVALID, "stream_id must be < 2^20");
+    HIP_TRY(hipSetDevice(c->device));
+    ldpc::GdbfArgs a;
+    gdbf_fill(a, c, cfg, batch);
+    a.src = ldpc::SRC_PHILOX;
+    const double N0 = std::pow(10.0, -ebn0_db / 10.0) / R;   // :175-176
+    a.sigma = std::sqrt(N0 / 2.0);
+    a.noise_sigma = a.sigma * cfg->noise_scale;               // :296
+    a.seed = seed;
+    a.stream_id = stream_id;
+    a.first_cw = first_cw;
+    a.cw_table = c->cw_rows ? (const int8_t *)c->cw_table.p : nullptr;
+    a.cw_rows = c->cw_rows;
+    a.frame_res = (int4 *)frames_dev;
+    return gdbf_run(c, a, cfg->precision == LDPC_F64);
+}
+
+int ldpc_gdbf_sim_launch(ldpc_ctx *c, double ebn0_db, double R, const ldpc_gdbf_cfg *cfg, uint64_t seed,
+                         uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames_dev)
+{
+    if (frames_dev && !is_device_ptr(frames_dev))
+        return set_err(LDPC_ERR_INVALID, "frames_dev must be a device pointer");
+    return gdbf_sim_impl(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, frames_dev);
+}
+
+int ldpc_gdbf_sim_batch(ldpc_ctx *c, double ebn0_db, double R, const ldpc_gdbf_cfg *cfg, uint64_t seed,
+                        uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames,
+                        ldpc_counts *accum)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    HIP_TRY(hipSetDevice(c->device));
+    ldpc_counts before;
+    int rc = read_counts(c, &before, 0);
+    if (rc) return rc;
+    const bool w_host = frames && !is_device_ptr(frames);
+    ldpc_frame_result *fw_dev = frames;
+    if (w_host) {
+        HIP_TRY(c->fw_stage.ensure(sizeof(ldpc_frame_result) * (size_t)std::max(batch, 1)));
+        fw_dev = (ldpc_frame_result *)c->fw_stage.p;
+    }
+    rc = gdbf_sim_impl(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, fw_dev);
+    if (rc) return rc;
+    if (w_host)
+        HIP_TRY(hipMemcpyAsync(frames, fw_dev, sizeof(ldpc_frame_result) * (size_t)batch, hipMemcpyDeviceToHost,
+                               c->stream));
+    return counts_delta(c, before, accum);
+}
+
+int ldpc_gdbf_kernel_info(ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, char *name, int name_len, int *lds_bytes)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    int rc = gdbf_check_cfg(cfg);
+    if (rc) return rc;
+    const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, cfg->precision == LDPC_F64);
+    if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", ch.name);
+    if (lds_bytes) *lds_bytes = ch.lds_bytes;
     return LDPC_OK;
 }
 

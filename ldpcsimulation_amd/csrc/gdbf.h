@@ -1,0 +1,37 @@
+// gdbf.h -- internal launch interface of the GDBF / NGDBF kernels (gdbf.hip).
+#pragma once
+#include "kernels.h"
+
+namespace ldpc {
+
+// The -D switches of src/decodeGDBF.cpp (values = LDPC_GDBF_* of ldpc_hip.h).
+enum { GDBF_NOISE = 1, GDBF_ADAPT = 2, GDBF_WEIGHT = 4, GDBF_SMOOTH = 8, GDBF_SATURATE = 16, GDBF_QUANTIZE = 32 };
+
+struct GdbfArgs {
+    int batch, T, flags, windowsize, src;
+    double theta0, lambda, w, noise_sigma, ymax, qmax, sigma;
+    const void *y;                  // SRC_GIVEN: raw channel samples [batch][N] (F)
+    const void *pert;               // SRC_GIVEN with GDBF_NOISE: perturbations [batch][T][N] (F)
+    const int8_t *c;                // SRC_GIVEN: bipolar codewords [batch][N] or null (+1)
+    const int8_t *cw_table;         // SRC_PHILOX: codeword table [cw_rows][N] or null
+    int cw_rows;
+    uint64_t seed, first_cw;
+    uint32_t stream_id;
+    int8_t *d_out;                  // [batch][N] or null
+    int4 *frame_res;                // [batch] {bit_err, uncoded, syndrome_fail, iterations} or null
+    unsigned long long *counts;     // [6] accumulated (iters = sum of iterations run)
+    unsigned long long *hist;       // [N] error-weight histogram
+};
+
+struct GdbfChoice {
+    const char *name = "";          // "gdbf_lds" | "gdbf_global"
+    int lds_bytes = 0, threads = 0;
+    size_t slot_bytes = 0;          // global kernel: state bytes per resident codeword
+};
+
+GdbfChoice gdbf_choose(const DevGraph &g, bool f64);
+// scratch: slots * choice.slot_bytes bytes for the global kernel (persistent grid of `slots`).
+hipError_t gdbf_launch(const DevGraph &g, const GdbfArgs &a, bool f64, const GdbfChoice &ch, void *scratch,
+                       int slots, hipStream_t s);
+
+}  // namespace ldpc

@@ -20,6 +20,7 @@
 // The translation unit is compiled with -ffp-contract=off (see Makefile):
 // no FMA may fuse the channel's 1 + sigma*n or the quantiser.
 #include "kernels.h"
+#include "device_common.h"
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -71,88 +72,12 @@ __device__ __forceinline__ F front_end(F y, const DecodeArgs &a)
     return q;
 }
 
-// ---------------------------------------------------------------------
-// Philox4x32-10 (Salmon et al. SC'11) + Box-Muller: 4 normals per call.
-// ---------------------------------------------------------------------
-__device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                              uint32_t k0, uint32_t k1, uint32_t out[4])
-{
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
-        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
-        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
-    }
-    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
-}
-
-// Uniforms in (0,1): (u + 1/2) * 2^-32.
-__device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, float &n0, float &n1)
-{
-    const float a = (float)ua * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
-    const float r = (float)ur * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
-    const float rad = sqrtf(-2.0f * logf(r));
-    float s, c;
-    sincospif(2.0f * a, &s, &c);
-    n0 = rad * c;
-    n1 = rad * s;
-}
-__device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, double &n0, double &n1)
-{
-    const double a = ((double)ua + 0.5) * 2.3283064365386963e-10;
-    const double r = ((double)ur + 0.5) * 2.3283064365386963e-10;
-    const double rad = sqrt(-2.0 * log(r));
-    double s, c;
-    sincospi(2.0 * a, &s, &c);
-    n0 = rad * c;
-    n1 = rad * s;
-}
-
 // Diagnostic phase timing (-DLDPC_STAMPS builds only; never in the shipped kernel).
 #ifdef LDPC_STAMPS
 #define STAMP(var) unsigned long long var = (threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0ull
 #else
 #define STAMP(var) [[maybe_unused]] constexpr unsigned long long var = 0ull
 #endif
-
-// Sum over the workgroup (64-wide waves, <= 16 waves).
-__device__ __forceinline__ int block_sum(int x, int *red)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    __syncthreads();
-    if (l == 0) red[w] = x;
-    __syncthreads();
-    int s = 0;
-    const int nw = (blockDim.x + 63) >> 6;
-    for (int i = 0; i < nw; ++i) s += red[i];
-    return s;
-}
-
-// Sums of NV values over the workgroup with one barrier pair; red holds 16*NV ints.
-template <int NV>
-__device__ __forceinline__ void block_sum_n(int (&x)[NV], int *red)
-{
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x[v] += __shfl_xor(x[v], o, 64);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = (blockDim.x + 63) >> 6;
-    __syncthreads();
-    if (l == 0)
-#pragma unroll
-        for (int v = 0; v < NV; ++v) red[w * NV + v] = x[v];
-    __syncthreads();
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        int t = 0;
-        for (int i = 0; i < nw; ++i) t += red[i * NV + v];
-        x[v] = t;
-    }
-}
 
 // ---------------------------------------------------------------------
 // One codeword, all T iterations. rows/app/yq may live in LDS or in a

@@ -22,7 +22,7 @@ LDPC_OK = 0
 MS, NMS, OMS = 0, 1, 2
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
@@ -44,7 +44,7 @@ class Counts(C.Structure):
 
 
 FRAME_DTYPE = np.dtype([("bit_err", np.int32), ("uncoded_bit_err", np.int32),
-                        ("syndrome_fail", np.int32), ("reserved", np.int32)])
+                        ("syndrome_fail", np.int32), ("iters", np.int32)])
 
 
 class _Cfg(C.Structure):
@@ -52,6 +52,42 @@ class _Cfg(C.Structure):
                 ("quantize", C.c_int32), ("saturate", C.c_int32), ("qbits", C.c_int32),
                 ("ymax", C.c_double), ("alpha", C.c_double), ("delta", C.c_double),
                 ("schedule", C.c_int32), ("reserved", C.c_int32)]
+
+
+GDBF_NOISE, GDBF_ADAPT, GDBF_WEIGHT, GDBF_SMOOTH, GDBF_SATURATE, GDBF_QUANTIZE = 1, 2, 4, 8, 16, 32
+# the reference's decodeGDBF.cpp Makefile targets (C_implementations/Makefile:33-53)
+GDBF_VARIANTS = {
+    "MNGDBF": GDBF_NOISE | GDBF_ADAPT | GDBF_WEIGHT | GDBF_SATURATE,
+    "SMNGDBF": GDBF_NOISE | GDBF_ADAPT | GDBF_WEIGHT | GDBF_SMOOTH | GDBF_SATURATE,
+    "ATGDBF": GDBF_ADAPT,
+    "SATGDBF": GDBF_ADAPT | GDBF_SMOOTH,
+    "SMGDBF": GDBF_SMOOTH,
+}
+
+
+class _GdbfCfg(C.Structure):
+    _fields_ = [("flags", C.c_int32), ("precision", C.c_int32), ("T", C.c_int32), ("windowsize", C.c_int32),
+                ("nq", C.c_int32), ("reserved", C.c_int32), ("theta", C.c_double), ("lambda_", C.c_double),
+                ("alpha", C.c_double), ("noise_scale", C.c_double), ("ymax", C.c_double)]
+
+
+@dataclass
+class GdbfConfig:
+    """GDBF / NGDBF bit flipping (src/decodeGDBF.cpp parallel mode); flags = the -D switches."""
+    flags: int = GDBF_VARIANTS["SMNGDBF"]
+    T: int = 100
+    theta: float = -0.6
+    lambda_: float = 0.99
+    alpha: float = 0.8
+    noise_scale: float = 0.75
+    ymax: float = 2.5
+    windowsize: int = 16
+    nq: int = 16
+    precision: int = 0   # F32
+
+    def _c(self) -> _GdbfCfg:
+        return _GdbfCfg(self.flags, self.precision, self.T, self.windowsize, self.nq, 0, self.theta, self.lambda_,
+                        self.alpha, self.noise_scale, self.ymax)
 
 
 @dataclass
@@ -108,6 +144,11 @@ def lib():
                            i32),
         "ldpc_ctx_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i32),
         "ldpc_ctx_kernel_info": ([vp, C.POINTER(_Cfg), C.c_char_p, i32, C.POINTER(i32), C.POINTER(i32)], i32),
+        "ldpc_gdbf_decode_batch": ([vp, vp, vp, i32, C.POINTER(_GdbfCfg), vp, vp, vp, C.POINTER(Counts)], i32),
+        "ldpc_gdbf_sim_launch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp], i32),
+        "ldpc_gdbf_sim_batch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp, C.POINTER(Counts)],
+                                i32),
+        "ldpc_gdbf_kernel_info": ([vp, C.POINTER(_GdbfCfg), C.c_char_p, i32, C.POINTER(i32)], i32),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)
@@ -124,7 +165,8 @@ EXPORTED = ["ldpc_abi_version", "ldpc_last_error", "ldpc_graph_create", "ldpc_gr
             "ldpc_graph_info", "ldpc_graph_destroy", "ldpc_graph_layers", "ldpc_device_count", "ldpc_ctx_create",
             "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
             "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",
-            "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info"]
+            "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info",
+            "ldpc_gdbf_decode_batch", "ldpc_gdbf_sim_launch", "ldpc_gdbf_sim_batch", "ldpc_gdbf_kernel_info"]
 
 
 def _check(rc: int):
@@ -293,3 +335,41 @@ class Context:
         lds, bpc = C.c_int(), C.c_int()
         _check(lib().ldpc_ctx_kernel_info(self._h, C.byref(cfg._c()), name, 32, C.byref(lds), C.byref(bpc)))
         return {"kernel": name.value.decode(), "lds_bytes": lds.value, "blocks_per_cu": bpc.value}
+
+    # ---- GDBF / NGDBF (src/decodeGDBF.cpp) ----
+    def gdbf_decode(self, y, pert, cfg: GdbfConfig, c=None, want_decisions: bool = True):
+        """Decode raw channel samples y[batch, N] with perturbations pert[batch, T, N] (or None
+        without GDBF_NOISE). Returns (d, frames (iters = iterations run), Counts)."""
+        N = self.graph.N
+        want = np.float64 if cfg.precision == F64 else np.float32
+        y = np.ascontiguousarray(y, dtype=want).reshape(-1, N)
+        batch = y.shape[0]
+        if pert is not None:
+            pert = np.ascontiguousarray(pert, dtype=want).reshape(batch, cfg.T, N)
+        if c is not None:
+            c = np.ascontiguousarray(c, dtype=np.int8)
+        d = np.empty((batch, N), dtype=np.int8) if want_decisions else None
+        fr = np.empty(batch, dtype=FRAME_DTYPE)
+        cnt = Counts()
+        _check(lib().ldpc_gdbf_decode_batch(self._h, _ptr(y), _ptr(pert), batch, C.byref(cfg._c()), _ptr(c),
+                                            _ptr(d), _ptr(fr), C.byref(cnt)))
+        return d, fr, cnt
+
+    def gdbf_sim_launch(self, ebn0_db: float, R: float, cfg: GdbfConfig, seed: int, stream_id: int, first_cw: int,
+                        batch: int, frames_dev=None):
+        _check(lib().ldpc_gdbf_sim_launch(self._h, ebn0_db, R, C.byref(cfg._c()), seed, stream_id, first_cw, batch,
+                                          _ptr(frames_dev)))
+
+    def gdbf_sim_batch(self, ebn0_db: float, R: float, cfg: GdbfConfig, seed: int, stream_id: int, first_cw: int,
+                       batch: int, want_frames: bool = True):
+        fr = np.empty(batch, dtype=FRAME_DTYPE) if want_frames else None
+        cnt = Counts()
+        _check(lib().ldpc_gdbf_sim_batch(self._h, ebn0_db, R, C.byref(cfg._c()), seed, stream_id, first_cw, batch,
+                                         _ptr(fr), C.byref(cnt)))
+        return fr, cnt
+
+    def gdbf_kernel_info(self, cfg: GdbfConfig) -> dict:
+        name = C.create_string_buffer(32)
+        lds = C.c_int()
+        _check(lib().ldpc_gdbf_kernel_info(self._h, C.byref(cfg._c()), name, 32, C.byref(lds)))
+        return {"kernel": name.value.decode(), "lds_bytes": lds.value}

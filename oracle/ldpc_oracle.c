@@ -60,6 +60,13 @@ double orc_rann(orc_rng *g)
     return cos(2.0 * 3.141592654 * u_angle) * sqrt(-2.0 * log(1.0 - u_rad));
 }
 
+/* n draws of scale * rann() in order (the perturbation rows of
+ * decodeGDBF.cpp:318-333: noiseSigma * rann() per bit and iteration). */
+void orc_rann_fill(orc_rng *g, long n, double scale, double *out)
+{
+    for (long i = 0; i < n; ++i) out[i] = scale * orc_rann(g);
+}
+
 /* ===================================================================== */
 /* alist reader: loadFile (src/alist.cpp:70-93): "N M", "maxdv maxdc",     */
 /* N column weights, M row weights, then N lines of maxdv and M lines of   */

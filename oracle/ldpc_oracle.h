@@ -36,6 +36,7 @@ void    orc_srandom(orc_rng *g, uint32_t seed);
 int32_t orc_random(orc_rng *g);
 double  orc_ranf(orc_rng *g);            /* rand.h:10-11 */
 double  orc_rann(orc_rng *g);            /* rand.h:19-20, cos operand drawn first */
+void    orc_rann_fill(orc_rng *g, long n, double scale, double *out);   /* out[i] = scale * rann() */
 
 /* ---- alist (reference loader semantics: fixed-width padded lines) ---- */
 typedef struct {

@@ -61,6 +61,7 @@ def lib():
         L.orc_ranf.restype = C.c_double
         L.orc_rann.argtypes = [C.POINTER(_Rng)]
         L.orc_rann.restype = C.c_double
+        L.orc_rann_fill.argtypes = [C.POINTER(_Rng), C.c_long, C.c_double, C.c_void_p]
         L.orc_alist_load.argtypes = [C.c_char_p, C.POINTER(_Alist)]
         L.orc_alist_free.argtypes = [C.POINTER(_Alist)]
         L.orc_minsum_run.argtypes = [C.POINTER(_Alist), C.c_double, C.c_double, C.c_int,
@@ -112,6 +113,16 @@ class GlibcRandom:
 
     def rann(self) -> float:
         return lib().orc_rann(C.byref(self._s))
+
+    def rann_fill(self, n: int, scale: float = 1.0) -> np.ndarray:
+        out = np.empty(n, dtype=np.float64)
+        lib().orc_rann_fill(C.byref(self._s), n, scale, out.ctypes.data)
+        return out
+
+    def copy(self) -> "GlibcRandom":
+        g = GlibcRandom.__new__(GlibcRandom)
+        g._s = _Rng.from_buffer_copy(self._s)
+        return g
 
     def channel(self, c: np.ndarray, sigma: float) -> np.ndarray:
         c = np.ascontiguousarray(c, dtype=np.int32)

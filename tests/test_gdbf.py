@@ -36,24 +36,26 @@ def test_oracle_reproduces_reference_gdbf_run(run):
 
 def _reference_frames(A, run, nframes):
     """Channel samples and perturbation rows of the first frames of a golden run, drawn
-    from the glibc restatement in the reference's order (:251-253, :318-333)."""
+    from the glibc restatement in the reference's order (:251-253, :318-333): y, then
+    one row of N perturbations per iteration that passes its syndrome check."""
     R, snr, c = gdbf_config(run)
     cfg = O.GdbfCfg(**c)
     g = O.GlibcRandom(run["seed"])
     sigma = math.sqrt(10 ** (-snr / 10) / R / 2)
+    lines = cw_lines(run)
     frames = []
-    for _ in range(nframes):
-        y = np.array([1.0 * (1.0 + sigma * g.rann()) for _ in range(A.N)])
-        state = O.GlibcRandom(0)
-        state._s = type(g._s).from_buffer_copy(g._s)
+    for f in range(nframes):
+        cw = np.ones(A.N, dtype=np.int32)
+        if lines:
+            cw = np.array([-1 if ch == "1" else 1 for ch in lines[f % len(lines)][:A.N]], dtype=np.int32)
+        y = g.channel(cw, sigma)
         pert = None
         if cfg.flags & O.GDBF_NOISE:
-            pert = np.array([sigma * cfg.noise_scale * state.rann() for _ in range(A.N * cfg.T)]).reshape(cfg.T, A.N)
+            pert = g.copy().rann_fill(A.N * cfg.T, sigma * cfg.noise_scale).reshape(cfg.T, A.N)
         d, it, sat = A.gdbf_decode(y, pert, cfg)
         if cfg.flags & O.GDBF_NOISE:
-            for _ in range(A.N * it):
-                g.rann()
-        frames.append((y, pert, d, it, sat))
+            g.rann_fill(A.N * it)
+        frames.append((y, pert, d, it, sat, cw))
     return cfg, frames
 
 
@@ -65,3 +67,120 @@ def test_oracle_frame_decode_matches_run():
     _, frames = _reference_frames(A, run, 6)
     assert [int((f[2] != 1).sum()) for f in frames] == list(fw)
     assert [f[3] for f in frames] == list(fi)
+
+
+# ------------------------------------------------------------------ GPU tier
+GPU_VARIANTS = {
+    "SMNGDBF": dict(flags=O.GDBF_NOISE | O.GDBF_ADAPT | O.GDBF_WEIGHT | O.GDBF_SMOOTH | O.GDBF_SATURATE),
+    "MNGDBF": dict(flags=O.GDBF_NOISE | O.GDBF_ADAPT | O.GDBF_WEIGHT | O.GDBF_SATURATE),
+    "ATGDBF": dict(flags=O.GDBF_ADAPT),
+    "SATGDBF": dict(flags=O.GDBF_ADAPT | O.GDBF_SMOOTH),
+    "QSMNGDBF": dict(flags=O.GDBF_NOISE | O.GDBF_ADAPT | O.GDBF_WEIGHT | O.GDBF_SMOOTH | O.GDBF_SATURATE
+                     | O.GDBF_QUANTIZE, nq=5),
+}
+COMMON = dict(T=60, theta=-0.6, lambda_=0.99, alpha=0.8, noise_scale=0.75, ymax=2.5, windowsize=16)
+
+
+def _gpu_cfg(native, c, f32):
+    return native.GdbfConfig(flags=c["flags"], T=c["T"], theta=c["theta"], lambda_=c["lambda_"], alpha=c["alpha"],
+                             noise_scale=c["noise_scale"], ymax=c["ymax"], windowsize=c["windowsize"],
+                             nq=c.get("nq", 16), precision=native.F32 if f32 else native.F64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("code", ["PEGReg504x1008.alist", "80211n_1944_r12.alist", "4000.2000.4.244.alist"])
+@pytest.mark.parametrize("vname", list(GPU_VARIANTS))
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_gdbf_decisions_bit_exact_vs_oracle(gpu_ctx_factory, code, vname, prec):
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(code)
+    A = O.Alist(code_path(code))
+    c = dict(COMMON, **GPU_VARIANTS[vname])
+    cfg = O.GdbfCfg(**c)
+    f32 = prec == "f32"
+    dt = np.float32 if f32 else np.float64
+    g = O.GlibcRandom(77 + len(vname))
+    B = 6
+    sigma = math.sqrt(10 ** (-3.0 / 10) / 0.5 / 2)
+    y = np.stack([g.channel(np.ones(A.N, dtype=np.int32), sigma) for _ in range(B)]).astype(dt)
+    pert = g.rann_fill(B * cfg.T * A.N, sigma * cfg.noise_scale).reshape(B, cfg.T, A.N).astype(dt)
+    d, fr, cnt = ctx.gdbf_decode(y, pert if cfg.flags & O.GDBF_NOISE else None, _gpu_cfg(native, c, f32))
+    its = []
+    for b in range(B):
+        want, it, sat = A.gdbf_decode(y[b], pert[b] if cfg.flags & O.GDBF_NOISE else None, cfg)
+        assert int((d[b] != want).sum()) == 0, b
+        assert fr["iters"][b] == it and fr["bit_err"][b] == int((want != 1).sum())
+        its.append(it)
+    assert cnt.iters == sum(its) and cnt.frames == B
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("run", golden_runs("gdbf"), ids=lambda r: r["name"])
+def test_gpu_reproduces_reference_gdbf_run(gpu_ctx_factory, run):
+    """The reference's own Monte-Carlo GDBF run, with its glibc channel and perturbations
+    (drawn on the host in the reference's order), decoded frame by frame on the GPU in fp64."""
+    from ldpcsimulation_amd import native
+    R, snr, c = gdbf_config(run)
+    cfg = O.GdbfCfg(**c)
+    gcfg = _gpu_cfg(native, c, False)
+    ctx = gpu_ctx_factory(run["code"], 64)
+    N = ctx.graph.N
+    g = O.GlibcRandom(run["seed"])
+    sigma = math.sqrt(10 ** (-snr / 10) / R / 2)
+    lines = cw_lines(run)
+    min_we = 20 if N <= 10000 else (10 if N <= 50000 else 5)
+    errors = words = word_errors = unc = iters = 0
+    ferr = []
+    while errors < 200 or word_errors < min_we:
+        cw = np.ones(N, dtype=np.int32)
+        if lines:
+            cw = np.array([-1 if ch == "1" else 1 for ch in lines[words % len(lines)][:N]], dtype=np.int32)
+        y = g.channel(cw, sigma)
+        pert = None
+        if cfg.flags & O.GDBF_NOISE:
+            pert = g.copy().rann_fill(N * cfg.T, sigma * cfg.noise_scale).reshape(1, cfg.T, N)
+        _, fr, _ = ctx.gdbf_decode(y[None], pert, gcfg, c=cw.astype(np.int8)[None], want_decisions=False)
+        it = int(fr["iters"][0])
+        if cfg.flags & O.GDBF_NOISE:
+            g.rann_fill(N * it)
+        unc += int(fr["uncoded_bit_err"][0])
+        iters += it
+        if fr["bit_err"][0] > 0:
+            errors += int(fr["bit_err"][0])
+            word_errors += 1
+            ferr.append(int(fr["bit_err"][0]))
+        words += 1
+    bit, nw, avg_it, unc_ref = gdbf_final_numbers(run["final"])
+    assert (errors, words, unc) == (bit, nw, unc_ref)
+    assert f"{iters / words:g}" == f"{avg_it:g}"
+    assert ferr == run["ferr_weights"]
+
+
+@pytest.mark.gpu
+def test_gdbf_sim_fer_matches_reference_statistically(gpu_ctx_factory):
+    """Config 4: SMNGDBF on 802.11n N=1944 at 3.5 dB with on-device Philox channel and
+    perturbations against the reference's golden run (two-proportion z-test |z| < 3)."""
+    from ldpcsimulation_amd import native
+    from ldpcsimulation_amd.sim import two_proportion_z
+    run = [r for r in golden_runs("gdbf") if r["name"] == "smngdbf_1944_3.5_T100_s9"][0]
+    R, snr, c = gdbf_config(run)
+    ctx = gpu_ctx_factory(run["code"], 8192)
+    fr, cnt = ctx.gdbf_sim_batch(snr, R, _gpu_cfg(native, c, True), seed=2027, stream_id=4, first_cw=0, batch=8192)
+    _, nw, avg_it, _ = gdbf_final_numbers(run["final"])
+    z = two_proportion_z(cnt.frame_err, cnt.frames, len(run["ferr_weights"]), nw)
+    assert abs(z) < 3, (cnt.frame_err, cnt.frames, z)
+    assert cnt.iters == int(fr["iters"].sum())
+    ok = fr["iters"] < c["T"]                      # early stop: all checks satisfied
+    assert (fr["syndrome_fail"][ok] == 0).all()
+    assert abs(cnt.iters / cnt.frames - avg_it) < 0.25 * avg_it
+
+
+@pytest.mark.gpu
+def test_gdbf_sim_independent_of_batch_split(gpu_ctx_factory):
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory("80211n_1944_r12.alist")
+    cfg = native.GdbfConfig(T=50)
+    full, _ = ctx.gdbf_sim_batch(3.0, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=300)
+    a, _ = ctx.gdbf_sim_batch(3.0, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=100)
+    b, _ = ctx.gdbf_sim_batch(3.0, 0.5, cfg, seed=5, stream_id=0, first_cw=100, batch=200)
+    assert np.array_equal(full, np.concatenate([a, b]))
