@@ -13,7 +13,8 @@ CXXFLAGS  = -O2 -std=c++17 -ffp-contract=off -Iinclude -Wall
 
 LIB       = $(LIBDIR)/libldpc_hip.so
 OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
-CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalizedMinSum $(BINDIR)/decodeOffsetMinSum
+CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalizedMinSum $(BINDIR)/decodeOffsetMinSum \
+            $(BINDIR)/decodeMNGDBF $(BINDIR)/decodeSMNGDBF $(BINDIR)/decodeATGDBF $(BINDIR)/decodeSATGDBF $(BINDIR)/decodeSMGDBF
 
 all: $(LIB) $(CLIS) oracle
 
@@ -49,6 +50,19 @@ $(BINDIR)/decodeNormalizedMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
 	g++ $(CXXFLAGS) -D quantizeSamples -D normalizedMS -o $@ $< $(CLI_LINK)
 $(BINDIR)/decodeOffsetMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
 	g++ $(CXXFLAGS) -D quantizeSamples -D offsetMS -o $@ $< $(CLI_LINK)
+
+# GDBF / NGDBF front-ends: the -D switches of C_implementations/Makefile:33-53.
+GDBF_SRC = $(CSRC)/cli_gdbf.cpp
+$(BINDIR)/decodeMNGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D addNoise -D thresholdAdaptation -D weightSyndromes -D saturateSamples -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeSMNGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D addNoise -D thresholdAdaptation -D weightSyndromes -D outputSmoothing -D saturateSamples -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeATGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D thresholdAdaptation -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeSATGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D thresholdAdaptation -D outputSmoothing -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeSMGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D outputSmoothing -o $@ $< $(CLI_LINK)
 
 # Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> lib/variants/libldpc_hip_x.so
 variant:

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--prec", default="f32")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--schedule", choices=["flooding", "layered"], default="flooding")
+    ap.add_argument("--decoder", choices=["minsum", "gdbf"], default="minsum",
+                    help="gdbf: SMNGDBF (theta -0.6, eta 0.75, lambda 0.99, w 0.8, window 16, Ymax 2.5)")
     a = ap.parse_args()
     g = native.Graph.from_alist(a.alist)
     ctx = native.Context(g, 0, a.batch)
@@ -31,17 +33,23 @@ def main():
          "oms": dict(variant=native.OMS, delta=0.15)}[a.variant]
     cfg = native.DecoderConfig(T=a.T, precision=native.F32 if a.prec == "f32" else native.F64,
                                schedule=native.LAYERED if a.schedule == "layered" else native.FLOODING, **v)
-    info = ctx.kernel_info(cfg)
-    ctx.sim_batch(a.snr, a.rate, cfg, seed=1, stream_id=0, first_cw=0, batch=a.batch)   # warm-up
+    if a.decoder == "gdbf":
+        cfg = native.GdbfConfig(T=a.T, precision=cfg.precision)
+        info = ctx.gdbf_kernel_info(cfg)
+        run = ctx.gdbf_sim_batch
+    else:
+        info = ctx.kernel_info(cfg)
+        run = ctx.sim_batch
+    run(a.snr, a.rate, cfg, seed=1, stream_id=0, first_cw=0, batch=a.batch)   # warm-up
     best = 1e30
     for r in range(a.reps):
         t0 = time.perf_counter()
-        _, cnt = ctx.sim_batch(a.snr, a.rate, cfg, seed=1, stream_id=0, first_cw=(r + 1) * a.batch, batch=a.batch)
+        _, cnt = run(a.snr, a.rate, cfg, seed=1, stream_id=0, first_cw=(r + 1) * a.batch, batch=a.batch)
         dt = time.perf_counter() - t0
         best = min(best, dt)
     mbit = g.N * a.batch / best / 1e6
     print(f"{os.path.basename(a.alist)} N={g.N} batch={a.batch} T={a.T} {a.variant}/{a.prec}: "
-          f"{a.schedule} {best*1e3:.1f} ms/batch  {mbit:.1f} Mbit/s  kernel={info}  last FER={cnt.frame_err}/{cnt.frames}")
+          f"{a.decoder}/{a.schedule} {best*1e3:.1f} ms/batch  {mbit:.1f} Mbit/s  kernel={info}  last FER={cnt.frame_err}/{cnt.frames}  avg it={cnt.iters / cnt.frames:.2f}")
 
 
 if __name__ == "__main__":

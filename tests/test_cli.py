@@ -34,6 +34,26 @@ def test_cli_stdout_identical_to_reference(tmp_path, run):
     assert log.read_text().replace(alist, "@ALIST@") == run["log_line"]
 
 
+@pytest.mark.parametrize("run", golden_runs("gdbf"), ids=lambda r: r["name"])
+def test_gdbf_cli_stdout_identical_to_reference(tmp_path, run):
+    """bin/decodeSMNGDBF & co. (cli_gdbf.cpp) print exactly what the reference's
+    decodeGDBF.cpp binaries printed for the same seed, and append the same log line."""
+    alist = code_path(run["code"])
+    log = tmp_path / "log.txt"
+    argv = [str(log) if a == "@LOG@" else a for a in run["args"]]
+    cmd = [os.path.join(BIN, run["binary"]), alist] + argv
+    if run["cwfile"]:
+        cmd.append(code_path(run["cwfile"]))
+    env = dict(os.environ, LDPC_SEED=str(run["seed"]), LDPC_RNG="glibc")
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr
+    out = p.stdout.replace(alist, "@ALIST@").replace(str(log), "@LOGFILE@")
+    if run["cwfile"]:
+        out = out.replace(code_path(run["cwfile"]), "@CWFILE@")
+    assert out == run["stdout"]
+    assert log.read_text().replace(alist, "@ALIST@") == run["log_line"]
+
+
 def test_cli_usage_exits_zero():
     p = subprocess.run([os.path.join(BIN, "decodeMinSum")], capture_output=True, text=True)
     assert p.returncode == 0
