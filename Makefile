@@ -12,9 +12,9 @@ HIPFLAGS  = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iincl
 CXXFLAGS  = -O2 -std=c++17 -ffp-contract=off -Iinclude -Wall
 
 LIB       = $(LIBDIR)/libldpc_hip.so
-OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
+OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
 CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalizedMinSum $(BINDIR)/decodeOffsetMinSum \
-            $(BINDIR)/decodeMNGDBF $(BINDIR)/decodeSMNGDBF $(BINDIR)/decodeATGDBF $(BINDIR)/decodeSATGDBF $(BINDIR)/decodeSMGDBF
+            $(BINDIR)/decodeMNGDBF $(BINDIR)/decodeSMNGDBF $(BINDIR)/decodeATGDBF $(BINDIR)/decodeSATGDBF $(BINDIR)/decodeSMGDBF $(BINDIR)/decodeBP
 
 all: $(LIB) $(CLIS) oracle
 
@@ -30,7 +30,9 @@ $(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h $(CSRC)/device_co
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
-$(LIBDIR)/obj/api.o: $(CSRC)/api.cpp $(CSRC)/kernels.h $(CSRC)/gdbf.h $(CSRC)/graph.h include/ldpc_hip.h | $(LIBDIR)/obj
+$(LIBDIR)/obj/bp.o: $(CSRC)/bp.hip $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+$(LIBDIR)/obj/api.o: $(CSRC)/api.cpp $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/gdbf.h $(CSRC)/graph.h include/ldpc_hip.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/graph.o: $(CSRC)/graph.cpp $(CSRC)/graph.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -51,6 +53,9 @@ $(BINDIR)/decodeNormalizedMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
 $(BINDIR)/decodeOffsetMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
 	g++ $(CXXFLAGS) -D quantizeSamples -D offsetMS -o $@ $< $(CLI_LINK)
 
+$(BINDIR)/decodeBP: $(CLI_SRC) $(LIB) | $(BINDIR)
+	g++ $(CXXFLAGS) -D beliefPropagation -o $@ $< $(CLI_LINK)
+
 # GDBF / NGDBF front-ends: the -D switches of C_implementations/Makefile:33-53.
 GDBF_SRC = $(CSRC)/cli_gdbf.cpp
 $(BINDIR)/decodeMNGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
@@ -70,7 +75,7 @@ variant:
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/api.o $(CSRC)/api.cpp
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/graph.o
+	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/graph.o
 
 oracle:
 	$(MAKE) -f oracle/Makefile

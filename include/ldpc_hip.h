@@ -23,6 +23,7 @@
  *   The compile-time variants of the reference (-D normalizedMS, offsetMS,
  *   quantizeSamples, saturateSamples; src/decodeMinSum.cpp:26-32,
  *   Makefile:58-65) are runtime fields of ldpc_decoder_cfg.
+ *   The belief-propagation decoder (src/decodeBP.cpp) is variant LDPC_BP.
  *   - ldpc_gdbf_decode_batch / ldpc_gdbf_sim_* replace the frame body of the
  *     GDBF / NGDBF bit-flipping decoders (src/decodeGDBF.cpp:250-399,
  *     checkNodeUpdates :517-534, symNodeUpdates :536-621), whose -D switches
@@ -45,7 +46,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 3
+#define LDPC_ABI_VERSION 4
 
 typedef enum {
     LDPC_OK = 0,
@@ -58,8 +59,11 @@ typedef enum {
 } ldpc_status;
 
 /* Check-node rule: MS = decodeMinSum, NMS = -D normalizedMS (c2v /= alpha,
- * src/decodeMinSum.cpp:494-499), OMS = -D offsetMS (:503-515). */
-typedef enum { LDPC_MS = 0, LDPC_NMS = 1, LDPC_OMS = 2 } ldpc_variant;
+ * src/decodeMinSum.cpp:494-499), OMS = -D offsetMS (:503-515), BP = the
+ * tanh rule of src/decodeBP.cpp (:353-409) with its LLR front-end
+ * yq = 4*y/n0 clipped to +-max_llr (:184-197; quantize/saturate ignored,
+ * flooding only). */
+typedef enum { LDPC_MS = 0, LDPC_NMS = 1, LDPC_OMS = 2, LDPC_BP = 3 } ldpc_variant;
 
 /* Message arithmetic. F64 is the reference's own precision and reproduces
  * its decisions bit-for-bit for identical y; F32 is the throughput path. */
@@ -107,6 +111,10 @@ typedef struct {
     double  delta;      /* OMS offset                                       */
     int32_t schedule;   /* ldpc_schedule (ABI 2)                            */
     int32_t reserved;   /* 0                                                */
+    double  n0;         /* BP: noise density N0 of the LLR front-end 4*y/N0 (ABI 4);
+                         * ldpc_decode_batch needs it > 0, the sim entry points
+                         * compute it from Eb/N0 and R (:104)               */
+    double  max_llr;    /* BP: MAXLLR message clip, 0 = the reference's 20 (:58) */
 } ldpc_decoder_cfg;
 
 int         ldpc_abi_version(void);

@@ -6,6 +6,7 @@
 // a message in ldpc_last_error().
 #include "ldpc_hip.h"
 #include "gdbf.h"
+#include "bp.h"
 
 #include <hip/hip_runtime.h>
 
@@ -403,7 +404,13 @@ static bool is_device_ptr(const void *p)
 static int check_cfg(const ldpc_ctx *c, const ldpc_decoder_cfg *cfg)
 {
     if (!cfg) return set_err(LDPC_ERR_INVALID, "cfg is null");
-    if (cfg->variant < LDPC_MS || cfg->variant > LDPC_OMS) return set_err(LDPC_ERR_INVALID, "bad variant %d", cfg->variant);
+    if (cfg->variant < LDPC_MS || cfg->variant > LDPC_BP) return set_err(LDPC_ERR_INVALID, "bad variant %d", cfg->variant);
+    if (cfg->variant == LDPC_BP) {
+        if (cfg->schedule != LDPC_FLOODING) return set_err(LDPC_ERR_UNSUPPORTED, "BP is flooding only");
+        if (c->g->maxdc > ldpc::kBpMaxDc)
+            return set_err(LDPC_ERR_UNSUPPORTED, "BP supports row degree <= %d", ldpc::kBpMaxDc);
+        if (cfg->max_llr < 0) return set_err(LDPC_ERR_INVALID, "max_llr must be >= 0");
+    }
     if (cfg->precision != LDPC_F32 && cfg->precision != LDPC_F64)
         return set_err(LDPC_ERR_INVALID, "bad precision %d", cfg->precision);
     if (cfg->T < 0) return set_err(LDPC_ERR_INVALID, "T must be >= 0");
@@ -430,6 +437,8 @@ static void fill_common(ldpc::DecodeArgs &a, ldpc_ctx *c, const ldpc_decoder_cfg
     a.nq = std::pow(2.0, (double)cfg->qbits);   // Nq = pow(2.0, Q) (:121)
     a.alpha = cfg->alpha;
     a.delta = cfg->delta;
+    a.n0 = cfg->n0;
+    a.max_llr = cfg->max_llr > 0 ? cfg->max_llr : 20.0;   // MAXLLR = 20 (decodeBP.cpp:58)
     a.counts = (unsigned long long *)c->counts.p;
     a.hist = (unsigned long long *)c->hist.p;
 }
@@ -465,8 +474,9 @@ static int nms_setup(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, ldpc::DecodeArgs 
     return LDPC_OK;
 }
 
-static ldpc::KernelChoice select_kernel(const ldpc_ctx *c, bool f64, int schedule)
+static ldpc::KernelChoice select_kernel(const ldpc_ctx *c, bool f64, int schedule, int variant)
 {
+    if (variant == LDPC_BP) return ldpc::bp_choose(c->dg, f64);
     if (schedule == LDPC_LAYERED)
         return ldpc::choose_layered(c->dg, f64, c->fs, c->ls, c->force[0] ? c->force : nullptr);
     return ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr,
@@ -477,8 +487,20 @@ static bool is_layered(const ldpc::KernelChoice &kc) { return kc.name[0] == 'l' 
 
 static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int schedule)
 {
-    const ldpc::KernelChoice kc = select_kernel(c, f64, schedule);
+    const ldpc::KernelChoice kc = select_kernel(c, f64, schedule, a.variant);
     const bool layered = is_layered(kc);
+    if (a.variant == ldpc::VARIANT_BP) {
+        int gblocks = 0;
+        if (kc.scratch_per_block) {
+            gblocks = std::min(a.batch, 4 * c->num_cus);
+            HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks));
+        }
+        HIP_TRY(hipEventRecord(c->ev0, c->stream));
+        HIP_TRY(ldpc::bp_launch(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream));
+        HIP_TRY(hipEventRecord(c->ev1, c->stream));
+        c->timed = true;
+        return LDPC_OK;
+    }
     int gblocks = layered ? c->num_cus : 0;
     if (kc.scratch_per_block) {
         int per_cu = layered ? ldpc::layered_blocks_per_cu(f64, kc) : ldpc::blocks_per_cu(c->dg, f64, kc);
@@ -568,6 +590,7 @@ int ldpc_decode_batch(ldpc_ctx *c, const void *y, int batch, const ldpc_decoder_
     if (batch <= 0 || batch > c->max_batch)
         return set_err(LDPC_ERR_INVALID, "batch %d outside 1..max_batch=%d", batch, c->max_batch);
     HIP_TRY(hipSetDevice(c->device));
+    if (cfg->variant == LDPC_BP && !(cfg->n0 > 0)) return set_err(LDPC_ERR_INVALID, "BP needs cfg->n0 > 0");
     const bool f64 = cfg->precision == LDPC_F64;
     const int N = c->g->N;
     const size_t ybytes = (size_t)batch * N * (f64 ? 8 : 4);
@@ -676,6 +699,7 @@ static int sim_launch_impl(ldpc_ctx *c, double ebn0_db, double R, const ldpc_dec
     }
     const double N0 = std::pow(10.0, -ebn0_db / 10.0) / R;   // :146
     a.sigma = std::sqrt(N0 / 2.0);                            // :147
+    if (cfg->variant == LDPC_BP) a.n0 = N0;                   // 4*y/N0 (decodeBP.cpp:104,188)
     a.seed = seed;
     a.stream_id = stream_id;
     a.first_cw = first_cw;
@@ -800,10 +824,10 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     const bool f64 = cfg->precision == LDPC_F64;
     int rc = check_cfg(c, cfg);
     if (rc) return rc;
-    const ldpc::KernelChoice kc = select_kernel(c, f64, cfg->schedule);
+    const ldpc::KernelChoice kc = select_kernel(c, f64, cfg->schedule, cfg->variant);
     if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", kc.name);
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
-    if (bpc) *bpc = is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
+    if (bpc) *bpc = cfg->variant == LDPC_BP ? 0 : is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
                                    : ldpc::blocks_per_cu(c->dg, f64, kc);
     return LDPC_OK;
 }

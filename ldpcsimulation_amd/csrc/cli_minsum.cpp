@@ -1,7 +1,10 @@
 // cli_minsum.cpp -- reference-compatible front-end of the MI355X decoder.
 //
 // Drop-in for the decodeMinSum family of ereiss123/LDPCsimulation
-// (C_implementations/src/decodeMinSum.cpp:72-334): the same positional CLI
+// (C_implementations/src/decodeMinSum.cpp:72-334) and, built with
+// -D beliefPropagation, for decodeBP (src/decodeBP.cpp:58-277: the tanh rule,
+// LLR front-end 4y/N0, stop rule 200 errors / 20|10|5 word errors, its own
+// parameter block and log line): the same positional CLI
 //   decodeMinSum alist R SNR T [Ymax] [Q] [alpha] [delta] logfilename [codewordfile]
 // with the variant fixed at compile time by the same -D macros
 // (quantizeSamples, saturateSamples, normalizedMS, offsetMS; Makefile:58-65),
@@ -95,6 +98,9 @@ int main(int argc, char *argv[])
 #endif
     args.push_back("logfilename");
     args.push_back("[codeword filename]");
+#ifdef beliefPropagation
+    args = {"alist", "R", "SNR", "T", "logfilename", "[codeword filename]"};   // decodeBP.cpp:60-67
+#endif
     if ((size_t)argc != args.size() && (size_t)argc != args.size() + 1) {   // :95-102
         cout << "Usage: " << argv[0];
         for (const auto &a : args) cout << " " << a;
@@ -105,6 +111,9 @@ int main(int argc, char *argv[])
     ldpc_decoder_cfg cfg;
     std::memset(&cfg, 0, sizeof cfg);
     cfg.variant = LDPC_MS;
+#ifdef beliefPropagation
+    cfg.variant = LDPC_BP;
+#endif
     int idx = 1;
     ldpc_graph *H = nullptr;
     if (ldpc_graph_load_alist(argv[idx++], &H) != LDPC_OK) die("loading alist");
@@ -168,7 +177,14 @@ int main(int argc, char *argv[])
     alist_header(argv[1], dv, dc);
     cout << "Simulating Min-Sum decoding on code with N=" << N << ", M=" << M << ", R=" << R << ", dv=" << dv
          << ", dc=" << dc << endl;
+#ifdef beliefPropagation
+    cout << "\nParameters are:\n\tSNR\t" << SNR << endl;   // decodeBP.cpp:114
+    cfg.n0 = N0;
+    const int minWordErrors = N > 50000 ? 5 : (N > 10000 ? 10 : 20);   // decodeBP.cpp:145-147
+#else
     cout << "\nParameters are:\n\tSNR\t" << SNR << "\n\tN0\t" << N0 << "\n\tsigma\t" << sigma << endl;
+    const int minWordErrors = 40;   // :189
+#endif
 
     // ---- GPU setup ----
     const std::string rng = env_or("LDPC_RNG", "glibc");
@@ -247,7 +263,7 @@ int main(int argc, char *argv[])
         }
         generated += batch;
         for (int f = 0; f < batch; ++f) {
-            if (!(errors < 200 || wordErrors < 40)) {   // :189
+            if (!(errors < 200 || wordErrors < minWordErrors)) {   // :189
                 done = true;
                 break;
             }

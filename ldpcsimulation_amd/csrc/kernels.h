@@ -14,10 +14,12 @@ struct DevGraph {
 };
 
 enum { SRC_GIVEN = 0, SRC_PHILOX = 1 };
+enum { VARIANT_BP = 3 };   // ldpc_variant LDPC_BP
 
 struct DecodeArgs {
     int batch, T, variant, quantize, saturate;
     double ymax, nq, alpha, delta;
+    double n0, max_llr;             // BP front-end: yq = 4*y/n0 clipped to +-max_llr
     // fp32 NMS: q = x*r, q += fma(-q, alpha, x)*r equals x/alpha for every
     // finite float x (verified on the device by verify_div_by_reciprocal)
     int nms_fast;

@@ -19,10 +19,10 @@ if os.environ.get("LDPC_LIB"):
     LIB_PATH = os.path.join(_PKG, "lib", "variants", f"libldpc_hip_{os.environ['LDPC_LIB']}.so")
 
 LDPC_OK = 0
-MS, NMS, OMS = 0, 1, 2
+MS, NMS, OMS, BP = 0, 1, 2, 3
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
@@ -51,7 +51,7 @@ class _Cfg(C.Structure):
     _fields_ = [("variant", C.c_int32), ("precision", C.c_int32), ("T", C.c_int32),
                 ("quantize", C.c_int32), ("saturate", C.c_int32), ("qbits", C.c_int32),
                 ("ymax", C.c_double), ("alpha", C.c_double), ("delta", C.c_double),
-                ("schedule", C.c_int32), ("reserved", C.c_int32)]
+                ("schedule", C.c_int32), ("reserved", C.c_int32), ("n0", C.c_double), ("max_llr", C.c_double)]
 
 
 GDBF_NOISE, GDBF_ADAPT, GDBF_WEIGHT, GDBF_SMOOTH, GDBF_SATURATE, GDBF_QUANTIZE = 1, 2, 4, 8, 16, 32
@@ -103,10 +103,12 @@ class DecoderConfig:
     ymax: float = 0.0
     qbits: int = 0
     schedule: int = FLOODING     # FLOODING (the reference's) | LAYERED (row-serial, config 3)
+    n0: float = 0.0              # BP (variant BP): N0 of the LLR front-end 4*y/N0 (decode only)
+    max_llr: float = 0.0         # BP: MAXLLR (0 = the reference's 20)
 
     def _c(self) -> _Cfg:
         return _Cfg(self.variant, self.precision, self.T, int(self.quantize), int(self.saturate),
-                    self.qbits, self.ymax, self.alpha, self.delta, self.schedule, 0)
+                    self.qbits, self.ymax, self.alpha, self.delta, self.schedule, 0, self.n0, self.max_llr)
 
 
 _lib = None

@@ -137,6 +137,18 @@ int64_t orc_gdbf_run(const orc_alist *H, double R, double snr, const orc_gdbf_cf
                      int32_t *frame_w, int32_t *frame_it, int64_t cap, orc_stats *out,
                      int64_t *smoothing_used);
 
+/* ---- belief propagation (src/decodeBP.cpp) ---- */
+/* front-end of one sample (:184-197): yq = 4y/N0 clipped to +-maxllr; *r = sgn(yq) */
+double orc_bp_front(double y, double N0, double maxllr, int *r);
+/* T flooding BP iterations on the front-end output yq (:199-213, :353-409);
+ * c2v_out (optional) receives the last c2v messages by (row, mlist position). */
+void orc_bp_decode_f64(const orc_alist *H, const double *yq, int T, double maxllr, int8_t *d, double *c2v_out);
+void orc_bp_decode_f32(const orc_alist *H, const float *yq, int T, double maxllr, int8_t *d, float *c2v_out);
+/* main() frame loop (:145-252), MAXLLR = 20, stop rule 200 / 20|10|5. */
+int64_t orc_bp_run(const orc_alist *H, double R, double snr, int T, uint32_t seed,
+                   const char *const *cw_lines, int ncw, int64_t max_frames,
+                   int32_t *frame_w, int64_t cap, orc_stats *out);
+
 /* Philox4x32-10 (Random123 reference constants). */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 

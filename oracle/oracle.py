@@ -94,6 +94,14 @@ def lib():
                                    C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                    C.POINTER(_Stats), C.POINTER(C.c_int64)]
         L.orc_gdbf_run.restype = C.c_int64
+        L.orc_bp_front.argtypes = [C.c_double, C.c_double, C.c_double, C.POINTER(C.c_int)]
+        L.orc_bp_front.restype = C.c_double
+        for name in ("orc_bp_decode_f64", "orc_bp_decode_f32"):
+            getattr(L, name).argtypes = [C.POINTER(_Alist), C.c_void_p, C.c_int, C.c_double, C.c_void_p,
+                                         C.c_void_p]
+        L.orc_bp_run.argtypes = [C.POINTER(_Alist), C.c_double, C.c_double, C.c_int, C.c_uint32, C.c_void_p,
+                                 C.c_int, C.c_int64, C.c_void_p, C.c_int64, C.POINTER(_Stats)]
+        L.orc_bp_run.restype = C.c_int64
         _LIB = L
     return _LIB
 
@@ -257,6 +265,37 @@ class Alist:
         k = min(n, cap)
         return n, {**{k2: getattr(st, k2) for k2, _ in _Stats._fields_}, "smoothing_used": su.value}, \
             fw[:k], fi[:k]
+
+    def bp_front(self, y: np.ndarray, N0: float, maxllr: float = 20.0) -> np.ndarray:
+        r = C.c_int()
+        return np.array([lib().orc_bp_front(float(v), N0, maxllr, C.byref(r)) for v in np.ravel(y)]).reshape(
+            np.shape(y))
+
+    def bp_decode(self, yq: np.ndarray, T: int, maxllr: float = 20.0, want_c2v: bool = False):
+        """BP decode of a [B, N] or [N] batch of front-end outputs (float64 or float32)."""
+        yq = np.ascontiguousarray(yq)
+        single = yq.ndim == 1
+        yq2 = yq.reshape(-1, self.N)
+        d = np.empty(yq2.shape, dtype=np.int8)
+        fn = lib().orc_bp_decode_f64 if yq2.dtype == np.float64 else lib().orc_bp_decode_f32
+        c2v = np.zeros((yq2.shape[0], self.M * max(self._a.maxdc, 1)), dtype=yq2.dtype) if want_c2v else None
+        for b in range(yq2.shape[0]):
+            fn(C.byref(self._a), yq2[b].ctypes.data, T, maxllr, d[b].ctypes.data,
+               c2v[b].ctypes.data if want_c2v else None)
+        d = d[0] if single else d
+        return (d, c2v) if want_c2v else d
+
+    def bp_run(self, R, snr, T, seed, cw_lines=None, max_frames=-1, cap=0):
+        st = _Stats()
+        fw = np.zeros(max(cap, 1), dtype=np.int32)
+        if cw_lines:
+            arr = (C.c_char_p * len(cw_lines))(*[s.encode() for s in cw_lines])
+            cwp, ncw = C.cast(arr, C.c_void_p), len(cw_lines)
+        else:
+            arr, cwp, ncw = None, None, 0
+        n = lib().orc_bp_run(C.byref(self._a), R, snr, T, seed & 0xFFFFFFFF, cwp, ncw, max_frames,
+                             fw.ctypes.data if cap else None, cap, C.byref(st))
+        return n, {k: getattr(st, k) for k, _ in _Stats._fields_}, fw[:min(n, cap)]
 
     def decode_snap(self, yq: np.ndarray, T: int, cfg: Cfg, snap_it: int):
         yq = np.ascontiguousarray(yq, dtype=np.float64)

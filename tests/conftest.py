@@ -35,10 +35,13 @@ def code_path(name: str) -> str:
 
 def golden_runs(kind: str = "minsum"):
     """Reference runs of tests/golden/reference_runs.json: kind "minsum" (decodeMinSum
-    family) or "gdbf" (decodeGDBF family)."""
+    family), "gdbf" (decodeGDBF family) or "bp" (decodeBP)."""
     with open(os.path.join(GOLD, "reference_runs.json")) as f:
         runs = json.load(f)["runs"]
-    return [r for r in runs if ("GDBF" in r["binary"]) == (kind == "gdbf")]
+
+    def kind_of(r):
+        return "gdbf" if "GDBF" in r["binary"] else ("bp" if r["binary"] == "decodeBP" else "minsum")
+    return [r for r in runs if kind_of(r) == kind]
 
 
 @pytest.fixture(scope="session")

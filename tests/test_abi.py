@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     L = native.lib()
-    assert L.ldpc_abi_version() == native.ABI_VERSION == 3
+    assert L.ldpc_abi_version() == native.ABI_VERSION == 4
     with pytest.raises(native.LdpcError) as e:
         native.Graph.from_alist("/nonexistent/file.alist")
     assert e.value.code == -5
@@ -74,6 +74,6 @@ def test_broken_reference_80211n_file_is_an_error_not_a_crash():
 
 
 def test_decoder_config_struct_layout():
-    assert C.sizeof(native._Cfg) == 6 * 4 + 3 * 8 + 2 * 4   # ABI 2: + schedule, reserved
+    assert C.sizeof(native._Cfg) == 6 * 4 + 3 * 8 + 2 * 4 + 2 * 8   # ABI 2: + schedule, reserved; ABI 4: + n0, max_llr
     assert C.sizeof(native.Counts) == 48
     assert native.FRAME_DTYPE.itemsize == 16

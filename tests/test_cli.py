@@ -54,6 +54,25 @@ def test_gdbf_cli_stdout_identical_to_reference(tmp_path, run):
     assert log.read_text().replace(alist, "@ALIST@") == run["log_line"]
 
 
+@pytest.mark.parametrize("run", golden_runs("bp"), ids=lambda r: r["name"])
+def test_bp_cli_stdout_identical_to_reference(tmp_path, run):
+    """bin/decodeBP (cli_minsum.cpp -D beliefPropagation) prints what the reference's
+    decodeBP printed for the same seed (fp64 on the GPU) and appends the same log line."""
+    alist = code_path(run["code"])
+    log = tmp_path / "log.txt"
+    cmd = [os.path.join(BIN, "decodeBP"), alist] + run["args"] + [str(log)]
+    if run["cwfile"]:
+        cmd.append(code_path(run["cwfile"]))
+    env = dict(os.environ, LDPC_SEED=str(run["seed"]), LDPC_RNG="glibc")
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr
+    out = p.stdout.replace(alist, "@ALIST@").replace(str(log), "@LOGFILE@")
+    if run["cwfile"]:
+        out = out.replace(code_path(run["cwfile"]), "@CWFILE@")
+    assert out == run["stdout"]
+    assert log.read_text().replace(alist, "@ALIST@") == run["log_line"]
+
+
 def test_cli_usage_exits_zero():
     p = subprocess.run([os.path.join(BIN, "decodeMinSum")], capture_output=True, text=True)
     assert p.returncode == 0

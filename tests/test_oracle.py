@@ -72,3 +72,15 @@ def test_oracle_decode_matches_frame_loop():
         y = g.channel(c, sigma)
         d = A.decode(y, 10, O.Cfg())
         assert int((d != 1).sum()) == fw[f]
+
+
+@pytest.mark.parametrize("run", golden_runs("bp"), ids=lambda r: r["name"])
+def test_oracle_reproduces_reference_bp_run(run):
+    """decodeBP (tanh-rule belief propagation, src/decodeBP.cpp) restated in
+    oracle/bp_oracle.c reproduces the reference's own runs frame by frame."""
+    R, snr, T = float(run["args"][0]), float(run["args"][1]), int(run["args"][2])
+    A = O.Alist(code_path(run["code"]))
+    n, st, fw = A.bp_run(R, snr, T, run["seed"], cw_lines=cw_lines(run), cap=200000)
+    bit, words, unc = final_numbers(run["final"])
+    assert (st["errors"], st["words"], st["uncoded"]) == (bit, words, unc)
+    assert [int(w) for w in fw if w > 0] == run["ferr_weights"]
