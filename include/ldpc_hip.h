@@ -28,6 +28,12 @@
  *     GDBF / NGDBF bit-flipping decoders (src/decodeGDBF.cpp:250-399,
  *     checkNodeUpdates :517-534, symNodeUpdates :536-621), whose -D switches
  *     (Makefile:33-53) are the flags of ldpc_gdbf_cfg.
+ *   - ldpc_nb_* / ldpc_ems_* (ABI 5): non-binary GF(16) codes (BASELINE
+ *     config 5). ldpc_nb_graph_create / _load_alist replace the NB-LDPC
+ *     model's loadFile() (SystemC/NB-LDPC/src/alist.cpp:23-56,
+ *     inc/alist.h:25-43: (index, GF value) pairs); the decode replaces its
+ *     symbol/check node iteration (inc/nodes.h:82-166, :240-293; a q^dc-LUT
+ *     BP there, which does not compile) with the Extended Min-Sum.
  *
  * Conventions: every function returns LDPC_OK (0) or a negative
  * ldpc_status; ldpc_last_error() gives a thread-local message. No C++
@@ -46,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 4
+#define LDPC_ABI_VERSION 5
 
 typedef enum {
     LDPC_OK = 0,
@@ -255,6 +261,70 @@ int  ldpc_gdbf_sim_batch(ldpc_ctx *ctx, double ebn0_db, double R, const ldpc_gdb
                          ldpc_counts *accum);
 /* Kernel chosen for a GDBF cfg ("gdbf_lds" / "gdbf_global") and its LDS bytes. */
 int  ldpc_gdbf_kernel_info(ldpc_ctx *ctx, const ldpc_gdbf_cfg *cfg, char *name, int name_len, int *lds_bytes);
+
+/* ---- non-binary GF(q) codes, Extended Min-Sum (BASELINE config 5) ------ */
+/* Messages are reliabilities over GF(q) (0 = most likely symbol); check
+ * nodes are the forward-backward EMS with messages truncated to the nm most
+ * likely symbols and absent symbols filled with (largest kept value +
+ * offset); symbol nodes add the channel reliabilities and the incoming
+ * messages. Channel: each symbol is m = log2(q) BPSK bits (bit i of the
+ * symbol's integer value, 0 -> +1), y = x(1 + sigma n), bit LLR 4y/N0.
+ * Exact definition: DESIGN.md §11 and oracle/ems_oracle.c. No reference
+ * counterpart computes this (parity unpinned); q = 2 reduces to min-sum. */
+typedef struct ldpc_nb_graph ldpc_nb_graph;
+typedef struct ldpc_nb_ctx ldpc_nb_ctx;
+
+typedef struct {
+    int32_t T;          /* maximum iterations                                */
+    int32_t nm;         /* message truncation (>= q: full vectors)           */
+    int32_t early_stop; /* stop when H*d = 0 (checked before each iteration)  */
+    int32_t reserved;   /* 0                                                 */
+    double  offset;     /* fill offset for truncated (absent) symbols        */
+} ldpc_ems_cfg;
+
+/* ldpc_counts + symbol errors; bit_err counts bits of the decided symbols. */
+typedef struct {
+    int64_t bit_err, frame_err, uncoded_bit_err, frames, iters, syndrome_fail, symbol_err;
+} ldpc_nb_counts;
+
+/* Arrays as the NB alist_struct (SystemC/NB-LDPC/inc/alist.h:25-43): nlist /
+ * nvals per column (1-based check, GF value), mlist / mvals per row. q a
+ * power of two (2..64), coefficients 1..q-1, check degree >= 2; both views
+ * must describe the same edges and coefficients (else LDPC_ERR_GRAPH). */
+int  ldpc_nb_graph_create(int N, int M, int q, const int *num_nlist, const int *const *nlist,
+                          const int *const *nvals, const int *num_mlist, const int *const *mlist,
+                          const int *const *mvals, ldpc_nb_graph **out);
+int  ldpc_nb_graph_load_alist(const char *path, ldpc_nb_graph **out);
+int  ldpc_nb_graph_info(const ldpc_nb_graph *g, int *N, int *M, int *q, int *E, int *maxdv, int *maxdc);
+void ldpc_nb_graph_destroy(ldpc_nb_graph *g);
+
+/* Device context (GF(16), row degree <= 16). */
+int  ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_nb_ctx **out);
+int  ldpc_nb_ctx_set_stream(ldpc_nb_ctx *ctx, void *hip_stream);
+void ldpc_nb_ctx_destroy(ldpc_nb_ctx *ctx);
+int  ldpc_nb_ctx_read_counts(ldpc_nb_ctx *ctx, ldpc_nb_counts *out, int reset);
+int  ldpc_nb_ctx_last_kernel_ms(ldpc_nb_ctx *ctx, float *ms);
+/* "ems_lds" (messages in LDS) or "ems_global" (a global slot per workgroup). */
+int  ldpc_ems_kernel_info(ldpc_nb_ctx *ctx, char *name, int name_len, int *lds_bytes);
+
+/* Decode given channel samples y[batch][N*m] (float, host or device) with
+ * bit LLRs 4y/n0. c: transmitted symbols [batch][N] or NULL (all-zero).
+ * d_out [batch][N] symbols, frames[].iters = iterations run. Synchronous. */
+int  ldpc_ems_decode_batch(ldpc_nb_ctx *ctx, const float *y, int batch, double n0, const ldpc_ems_cfg *cfg,
+                           const uint8_t *c, uint8_t *d_out, ldpc_frame_result *frames, ldpc_nb_counts *counts);
+/* Fused Monte-Carlo of the all-zero codeword: Philox4x32-10 keyed by
+ * (seed; symbol, frame, stream_id), sigma = sqrt(10^(-ebn0/10)/R/2).
+ * Asynchronous; counts accumulate in the context. */
+int  ldpc_ems_sim_launch(ldpc_nb_ctx *ctx, double ebn0_db, double R, const ldpc_ems_cfg *cfg, uint64_t seed,
+                         uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames_dev);
+int  ldpc_ems_sim_batch(ldpc_nb_ctx *ctx, double ebn0_db, double R, const ldpc_ems_cfg *cfg, uint64_t seed,
+                        uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames,
+                        ldpc_nb_counts *accum);
+/* ldpc_ems_sim_batch that also returns the generated samples y_out [batch][N*m]
+ * and decisions d_out [batch][N] (host or device; either may be NULL). */
+int  ldpc_ems_sim_trace(ldpc_nb_ctx *ctx, double ebn0_db, double R, const ldpc_ems_cfg *cfg, uint64_t seed,
+                        uint32_t stream_id, uint64_t first_cw, int batch, float *y_out, uint8_t *d_out,
+                        ldpc_frame_result *frames, ldpc_nb_counts *accum);
 
 #ifdef __cplusplus
 }

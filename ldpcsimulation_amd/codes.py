@@ -205,3 +205,184 @@ def has_4cycle(H: ParityCheck) -> bool:
                     return True
                 seen.add(key)
     return False
+
+
+# --------------------------------------------------------------------------
+# Non-binary (GF(q)) codes: the NB alist of SystemC/NB-LDPC/src/alist.cpp:23-56
+# ("N M q", "maxdv maxdc", column weights, row weights, then per column
+# maxdv (row, value) pairs and per row maxdc (column, value) pairs, 1-based,
+# zero-padded with "0 0"), and the GF(16) code of BASELINE config 5, which the
+# reference does not hold (its NB codes are GF(2/4/8), N = 6000-9000).
+# --------------------------------------------------------------------------
+GF_POLY = {2: 0x3, 4: 0x7, 8: 0xB, 16: 0x13, 32: 0x25, 64: 0x43}   # primitive polynomials
+
+
+def gf_mul(q: int, a: int, b: int) -> int:
+    """a*b in GF(q), q = 2^m, polynomial basis over GF_POLY[q]."""
+    poly, r = GF_POLY[q], 0
+    while b:
+        if b & 1:
+            r ^= a
+        b >>= 1
+        a <<= 1
+        if a & q:
+            a ^= poly
+    return r
+
+
+def gf_inv(q: int, a: int) -> int:
+    return next(b for b in range(1, q) if gf_mul(q, a, b) == 1)
+
+
+@dataclass
+class NbParityCheck:
+    """H over GF(q): rows[j] = [(col, h), ...] in mlist order, cols[i] = [(row, h), ...] in nlist order."""
+    N: int
+    M: int
+    q: int
+    rows: List[List[tuple]]
+    cols: List[List[tuple]]
+
+    @property
+    def E(self) -> int:
+        return sum(len(r) for r in self.rows)
+
+    def csr(self):
+        """Device/oracle layout: row_ptr[M+1], row_col[E], row_h[E] (edge slot = row_ptr[j] + k),
+        col_ptr[N+1], col_slot[E] (each symbol's edge slots in nlist order)."""
+        import numpy as np
+        row_ptr = np.zeros(self.M + 1, dtype=np.int32)
+        for j, r in enumerate(self.rows):
+            row_ptr[j + 1] = row_ptr[j] + len(r)
+        row_col = np.array([c for r in self.rows for c, _ in r], dtype=np.int32)
+        row_h = np.array([h for r in self.rows for _, h in r], dtype=np.int32)
+        col_ptr = np.zeros(self.N + 1, dtype=np.int32)
+        slots = []
+        for i, c in enumerate(self.cols):
+            col_ptr[i + 1] = col_ptr[i] + len(c)
+            for j, _ in c:
+                k = max(k for k, (cc, _) in enumerate(self.rows[j]) if cc == i)
+                slots.append(int(row_ptr[j]) + k)
+        return row_ptr, row_col, row_h, col_ptr, np.array(slots, dtype=np.int32)
+
+    def syndrome(self, d) -> List[int]:
+        out = []
+        for r in self.rows:
+            s = 0
+            for c, h in r:
+                s ^= gf_mul(self.q, h, int(d[c]))
+            out.append(s)
+        return out
+
+
+def nb_alist_text(H: NbParityCheck) -> str:
+    dv = max(len(c) for c in H.cols)
+    dc = max(len(r) for r in H.rows)
+    out = [f"{H.N} {H.M} {H.q}", f"{dv} {dc}",
+           " ".join(str(len(c)) for c in H.cols), " ".join(str(len(r)) for r in H.rows)]
+    for c in H.cols:
+        out.append(" ".join(f"{j + 1} {h}" for j, h in c) + " 0 0" * (dv - len(c)))
+    for r in H.rows:
+        out.append(" ".join(f"{i + 1} {h}" for i, h in r) + " 0 0" * (dc - len(r)))
+    return "\n".join(out) + "\n"
+
+
+def read_nb_alist(path: str) -> NbParityCheck:
+    """NB alist with loadFile's semantics (SystemC/NB-LDPC/src/alist.cpp:29-53): whitespace-separated
+    integers, fixed maxdv / maxdc pairs per line, (0, 0) padding; validated (both views agree)."""
+    with open(path) as f:
+        tok = [int(x) for x in f.read().split()]
+    N, M, q, dv, dc = tok[:5]
+    p = 5
+    wn, p = tok[p:p + N], p + N
+    wm, p = tok[p:p + M], p + M
+    cols, rows = [], []
+    for i in range(N):
+        pr = tok[p:p + 2 * dv]
+        p += 2 * dv
+        cols.append([(pr[2 * k] - 1, pr[2 * k + 1]) for k in range(wn[i])])
+    for j in range(M):
+        pr = tok[p:p + 2 * dc]
+        p += 2 * dc
+        rows.append([(pr[2 * k] - 1, pr[2 * k + 1]) for k in range(wm[j])])
+    H = NbParityCheck(N, M, q, rows, cols)
+    a = sorted((j, i, h) for i, c in enumerate(cols) for j, h in c)
+    b = sorted((j, i, h) for j, r in enumerate(rows) for i, h in r)
+    if a != b:
+        raise ValueError(f"{path}: column and row views disagree")
+    if any(not (0 < h < q) for _, _, h in a):
+        raise ValueError(f"{path}: coefficient outside 1..q-1")
+    return H
+
+
+def peg_nb_code(N: int, M: int, dv: int, q: int, seed: int) -> NbParityCheck:
+    """Progressive-edge-growth (Hu, Eleftheriou, Arnold 2005) Tanner graph with
+    column weight dv and row weight capped at ceil(N*dv/M) (so a dv*N = dc*M
+    code comes out regular): each new edge of a symbol goes to a check of the
+    greatest graph distance from it (unreachable first), then lowest degree,
+    ties broken by a seeded RNG; nonzero GF(q) coefficients are drawn
+    uniformly from the same RNG."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    cap = -(-N * dv // M)
+    chk = [[] for _ in range(M)]
+    var = [[] for _ in range(N)]
+    deg = np.zeros(M, dtype=np.int64)
+    big = 1 << 30
+    for v in range(N):
+        for _ in range(dv):
+            depth = np.full(M, big, dtype=np.int64)   # distance in check layers from v
+            seen_v = np.zeros(N, dtype=bool)
+            seen_v[v] = True
+            frontier, lvl = [v], 0
+            while frontier:
+                nc = [c for u in frontier for c in var[u] if depth[c] == big]
+                nc = list(dict.fromkeys(nc))
+                if not nc:
+                    break
+                depth[nc] = lvl
+                nv = list(dict.fromkeys(u for c in nc for u in chk[c] if not seen_v[u]))
+                seen_v[nv] = True
+                frontier, lvl = nv, lvl + 1
+            ok = np.flatnonzero((deg < cap) & ~np.isin(np.arange(M), var[v]))
+            pool = ok[depth[ok] == depth[ok].max()]
+            pool = pool[deg[pool] == deg[pool].min()]
+            c = int(rng.choice(pool))
+            chk[c].append(v)
+            var[v].append(c)
+            deg[c] += 1
+    h = {}
+    for v in range(N):
+        for c in var[v]:
+            h[(c, v)] = int(rng.integers(1, q))
+    rows = [[(v, h[(c, v)]) for v in sorted(chk[c])] for c in range(M)]
+    cols = [[(c, h[(c, v)]) for c in sorted(var[v])] for v in range(N)]
+    return NbParityCheck(N, M, q, rows, cols)
+
+
+GF16_CODE = "gf16_N1000_dv2_dc4.alist"   # BASELINE config 5: N = 1000 GF(16) symbols, rate 1/2
+
+
+def ensure_gf16_code() -> str:
+    """Path of the config-5 code (codes/gf16_N1000_dv2_dc4.alist), generated by peg_nb_code(seed=16)."""
+    path = os.path.join(codes_dir(), GF16_CODE)
+    if not os.path.exists(path):
+        txt = nb_alist_text(peg_nb_code(1000, 500, 2, 16, seed=16))
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
+            f.write(txt)
+        os.replace(tmp, path)
+    return path
+
+
+def nb_girth_at_least_6(H: NbParityCheck) -> bool:
+    """No two checks share two symbols (no 4-cycles)."""
+    seen = set()
+    for r in H.rows:
+        cs = sorted(c for c, _ in r)
+        for a in range(len(cs)):
+            for b in range(a + 1, len(cs)):
+                if (cs[a], cs[b]) in seen:
+                    return False
+                seen.add((cs[a], cs[b]))
+    return True

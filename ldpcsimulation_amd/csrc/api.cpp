@@ -7,6 +7,7 @@
 #include "ldpc_hip.h"
 #include "gdbf.h"
 #include "bp.h"
+#include "nb.h"
 
 #include <hip/hip_runtime.h>
 
@@ -91,6 +92,14 @@ struct ldpc_ctx {
     DevBuf divcheck;                                      // mismatch counter of verify_div_by_reciprocal
     std::vector<std::pair<float, bool>> div_ok;           // alpha -> reciprocal division exact
 };
+
+namespace ldpc {
+int set_last_error(int code, const std::string &msg)
+{
+    g_last_error = msg;
+    return code;
+}
+}  // namespace ldpc
 
 extern "C" {
 

@@ -1,0 +1,577 @@
+// nb_api.cpp -- C ABI of the non-binary GF(q) EMS decoder (include/ldpc_hip.h,
+// "non-binary" section): NB alist loading with the semantics of the
+// reference's SystemC/NB-LDPC/src/alist.cpp:23-56 (plus validation), device
+// contexts, decode of given channel samples and the fused Monte-Carlo.
+#include "ldpc_hip.h"
+#include "nb.h"
+#include "kernels.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+namespace {
+
+int err(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int err(int code, const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    return ldpc::set_last_error(code, buf);
+}
+
+#define NB_HIP_TRY(expr)                                                                                   \
+    do {                                                                                                   \
+        hipError_t e_ = (expr);                                                                            \
+        if (e_ != hipSuccess) {                                                                            \
+            (void)hipGetLastError();                                                                       \
+            return err(LDPC_ERR_DEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                       __LINE__);                                                                          \
+        }                                                                                                  \
+    } while (0)
+
+struct Buf {
+    void *p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes)
+    {
+        if (bytes <= n) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) n = bytes;
+        return e;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+int gf_poly(int q)
+{
+    switch (q) {
+    case 2: return 0x3;
+    case 4: return 0x7;
+    case 8: return 0xB;
+    case 16: return 0x13;
+    case 32: return 0x25;
+    case 64: return 0x43;
+    default: return 0;
+    }
+}
+
+int gf_mul(int q, int a, int b)
+{
+    const int poly = gf_poly(q);
+    int r = 0;
+    while (b) {
+        if (b & 1) r ^= a;
+        b >>= 1;
+        a <<= 1;
+        if (a & q) a ^= poly;
+    }
+    return r;
+}
+
+bool is_device_ptr(const void *p)
+{
+    if (!p) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+
+}  // namespace
+
+struct ldpc_nb_graph {
+    int N = 0, M = 0, q = 0, m = 0, E = 0, maxdv = 0, maxdc = 0;
+    std::vector<int32_t> row_ptr, row_col, col_ptr, col_slot;
+    std::vector<uint8_t> row_h;
+};
+
+struct ldpc_nb_ctx {
+    int device = 0, max_batch = 0, num_cus = 0;
+    const ldpc_nb_graph *g = nullptr;
+    hipStream_t own = nullptr, stream = nullptr;
+    ldpc::NbDevGraph dg{};
+    Buf graph, counts, y_stage, c_stage, d_stage, fr_stage, scratch;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+};
+
+// Build the CSR views from (row, value) lists per column and (column, value) per row (0-based).
+static int build_nb(int N, int M, int q, const std::vector<std::vector<std::pair<int, int>>> &cols,
+                    const std::vector<std::vector<std::pair<int, int>>> &rows, ldpc_nb_graph &g)
+{
+    if (N <= 0 || M <= 0) return err(LDPC_ERR_GRAPH, "bad dimensions N=%d M=%d", N, M);
+    if (!gf_poly(q)) return err(LDPC_ERR_GRAPH, "q=%d is not a supported power of two (2..64)", q);
+    g.N = N;
+    g.M = M;
+    g.q = q;
+    g.m = 0;
+    while ((1 << g.m) < q) ++g.m;
+    g.row_ptr.assign(M + 1, 0);
+    for (int j = 0; j < M; ++j) {
+        if (rows[j].size() < 2) return err(LDPC_ERR_GRAPH, "check %d has degree %zu (< 2)", j, rows[j].size());
+        g.row_ptr[j + 1] = g.row_ptr[j] + (int)rows[j].size();
+        g.maxdc = std::max(g.maxdc, (int)rows[j].size());
+    }
+    g.E = g.row_ptr[M];
+    g.row_col.resize(g.E);
+    g.row_h.resize(g.E);
+    std::vector<std::vector<std::pair<int, int>>> seen(N);   // (row, h) pairs from the row view
+    for (int j = 0; j < M; ++j)
+        for (size_t k = 0; k < rows[j].size(); ++k) {
+            const int c = rows[j][k].first, h = rows[j][k].second;
+            if (c < 0 || c >= N) return err(LDPC_ERR_GRAPH, "check %d: symbol index %d out of range", j, c + 1);
+            if (h <= 0 || h >= q) return err(LDPC_ERR_GRAPH, "check %d: coefficient %d outside 1..q-1", j, h);
+            for (const auto &pr : seen[c])
+                if (pr.first == j) return err(LDPC_ERR_GRAPH, "check %d lists symbol %d twice", j, c + 1);
+            g.row_col[g.row_ptr[j] + k] = c;
+            g.row_h[g.row_ptr[j] + k] = (uint8_t)h;
+            seen[c].push_back({j, (int)(g.row_ptr[j] + k)});
+        }
+    g.col_ptr.assign(N + 1, 0);
+    g.col_slot.clear();
+    g.col_slot.reserve(g.E);
+    for (int i = 0; i < N; ++i) {
+        if (cols[i].size() != seen[i].size())
+            return err(LDPC_ERR_GRAPH, "symbol %d: column weight %zu but %zu rows list it", i + 1, cols[i].size(),
+                       seen[i].size());
+        for (const auto &ce : cols[i]) {
+            const int j = ce.first;
+            int slot = -1;
+            for (const auto &pr : seen[i])
+                if (pr.first == j) slot = pr.second;
+            if (slot < 0) return err(LDPC_ERR_GRAPH, "symbol %d lists check %d, which does not list it", i + 1, j + 1);
+            if (g.row_h[slot] != ce.second)
+                return err(LDPC_ERR_GRAPH, "edge (%d,%d): coefficient %d in the column view, %d in the row view",
+                           j + 1, i + 1, ce.second, g.row_h[slot]);
+            g.col_slot.push_back(slot);
+        }
+        g.col_ptr[i + 1] = (int)g.col_slot.size();
+        g.maxdv = std::max(g.maxdv, (int)cols[i].size());
+    }
+    return LDPC_OK;
+}
+
+extern "C" {
+
+int ldpc_nb_graph_create(int N, int M, int q, const int *num_nlist, const int *const *nlist, const int *const *nvals,
+                         const int *num_mlist, const int *const *mlist, const int *const *mvals, ldpc_nb_graph **out)
+{
+    if (!out || !num_nlist || !nlist || !nvals || !num_mlist || !mlist || !mvals)
+        return err(LDPC_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (N <= 0 || M <= 0) return err(LDPC_ERR_GRAPH, "bad dimensions N=%d M=%d", N, M);
+    try {
+        std::vector<std::vector<std::pair<int, int>>> cols(N), rows(M);
+        for (int i = 0; i < N; ++i)
+            for (int k = 0; k < num_nlist[i]; ++k) cols[i].push_back({nlist[i][k] - 1, nvals[i][k]});
+        for (int j = 0; j < M; ++j)
+            for (int k = 0; k < num_mlist[j]; ++k) rows[j].push_back({mlist[j][k] - 1, mvals[j][k]});
+        auto *g = new ldpc_nb_graph();
+        const int rc = build_nb(N, M, q, cols, rows, *g);
+        if (rc) {
+            delete g;
+            return rc;
+        }
+        *out = g;
+    } catch (const std::bad_alloc &) {
+        return err(LDPC_ERR_NOMEM, "graph build out of memory");
+    }
+    return LDPC_OK;
+}
+
+int ldpc_nb_graph_load_alist(const char *path, ldpc_nb_graph **out)
+{
+    if (!path || !out) return err(LDPC_ERR_INVALID, "null argument");
+    *out = nullptr;
+    FILE *f = std::fopen(path, "r");
+    if (!f) return err(LDPC_ERR_IO, "cannot open %s", path);
+    auto rd = [&](int &v) { return std::fscanf(f, "%d", &v) == 1; };
+    int N = 0, M = 0, q = 0, dv = 0, dc = 0;
+    if (!rd(N) || !rd(M) || !rd(q) || !rd(dv) || !rd(dc) || N <= 0 || M <= 0 || dv <= 0 || dc <= 0 ||
+        N > (1 << 26) || M > (1 << 26) || dv > 1024 || dc > 1024) {
+        std::fclose(f);
+        return err(LDPC_ERR_GRAPH, "%s: bad NB alist header", path);
+    }
+    try {
+        std::vector<int> wn(N), wm(M);
+        bool ok = true;
+        for (int i = 0; i < N && ok; ++i) ok = rd(wn[i]) && wn[i] >= 0 && wn[i] <= dv;
+        for (int j = 0; j < M && ok; ++j) ok = rd(wm[j]) && wm[j] >= 0 && wm[j] <= dc;
+        std::vector<std::vector<std::pair<int, int>>> cols(N), rows(M);
+        for (int i = 0; i < N && ok; ++i)
+            for (int k = 0; k < dv && ok; ++k) {
+                int a = 0, b = 0;
+                ok = rd(a) && rd(b);
+                if (k < wn[i]) cols[i].push_back({a - 1, b});
+            }
+        for (int j = 0; j < M && ok; ++j)
+            for (int k = 0; k < dc && ok; ++k) {
+                int a = 0, b = 0;
+                ok = rd(a) && rd(b);
+                if (k < wm[j]) rows[j].push_back({a - 1, b});
+            }
+        std::fclose(f);
+        if (!ok) return err(LDPC_ERR_GRAPH, "%s: truncated or malformed NB alist", path);
+        auto *g = new ldpc_nb_graph();
+        const int rc = build_nb(N, M, q, cols, rows, *g);
+        if (rc) {
+            delete g;
+            return rc;
+        }
+        *out = g;
+    } catch (const std::bad_alloc &) {
+        return err(LDPC_ERR_NOMEM, "alist load out of memory");
+    }
+    return LDPC_OK;
+}
+
+int ldpc_nb_graph_info(const ldpc_nb_graph *g, int *N, int *M, int *q, int *E, int *maxdv, int *maxdc)
+{
+    if (!g) return err(LDPC_ERR_INVALID, "graph is null");
+    if (N) *N = g->N;
+    if (M) *M = g->M;
+    if (q) *q = g->q;
+    if (E) *E = g->E;
+    if (maxdv) *maxdv = g->maxdv;
+    if (maxdc) *maxdc = g->maxdc;
+    return LDPC_OK;
+}
+
+void ldpc_nb_graph_destroy(ldpc_nb_graph *g) { delete g; }
+
+int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_nb_ctx **out)
+{
+    if (!g || !out) return err(LDPC_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (max_batch <= 0) return err(LDPC_ERR_INVALID, "max_batch must be > 0");
+    if (g->q != ldpc::kNbQ) return err(LDPC_ERR_UNSUPPORTED, "the EMS kernels are built for GF(16), got q=%d", g->q);
+    if (g->maxdc > ldpc::kNbMaxDc) return err(LDPC_ERR_UNSUPPORTED, "row degree %d > %d", g->maxdc, ldpc::kNbMaxDc);
+    int ndev = 0;
+    NB_HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return err(LDPC_ERR_INVALID, "device %d outside 0..%d", device, ndev - 1);
+    NB_HIP_TRY(hipSetDevice(device));
+    auto *c = new (std::nothrow) ldpc_nb_ctx();
+    if (!c) return err(LDPC_ERR_NOMEM, "context allocation failed");
+    c->device = device;
+    c->max_batch = max_batch;
+    c->g = g;
+    hipDeviceProp_t prop;
+    NB_HIP_TRY(hipGetDeviceProperties(&prop, device));
+    c->num_cus = prop.multiProcessorCount;
+    NB_HIP_TRY(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking));
+    c->stream = c->own;
+    NB_HIP_TRY(hipEventCreate(&c->ev0));
+    NB_HIP_TRY(hipEventCreate(&c->ev1));
+    // graph upload: row_ptr | row_col | col_ptr | col_slot | row_h | gf_mul | gf_inv
+    const int q = g->q;
+    std::vector<uint8_t> mul((size_t)q * q), inv(q, 0);
+    for (int a = 0; a < q; ++a)
+        for (int b = 0; b < q; ++b) {
+            mul[(size_t)a * q + b] = (uint8_t)gf_mul(q, a, b);
+            if (mul[(size_t)a * q + b] == 1) inv[a] = (uint8_t)b;
+        }
+    const size_t n_rp = (g->M + 1) * 4, n_rc = (size_t)g->E * 4, n_cp = (g->N + 1) * 4, n_cs = (size_t)g->E * 4;
+    const size_t total = n_rp + n_rc + n_cp + n_cs + g->E + mul.size() + inv.size() + 64;
+    std::vector<uint8_t> blob(total, 0);
+    size_t off = 0;
+    auto put = [&](const void *src, size_t n) {
+        const size_t o = off;
+        std::memcpy(blob.data() + off, src, n);
+        off = (off + n + 15) & ~(size_t)15;
+        return o;
+    };
+    blob.resize(total + 256);
+    const size_t o_rp = put(g->row_ptr.data(), n_rp), o_rc = put(g->row_col.data(), n_rc),
+                 o_cp = put(g->col_ptr.data(), n_cp), o_cs = put(g->col_slot.data(), n_cs),
+                 o_h = put(g->row_h.data(), g->E), o_mul = put(mul.data(), mul.size()),
+                 o_inv = put(inv.data(), inv.size());
+    NB_HIP_TRY(c->graph.ensure(off));
+    NB_HIP_TRY(hipMemcpy(c->graph.p, blob.data(), off, hipMemcpyHostToDevice));
+    auto *base = (uint8_t *)c->graph.p;
+    c->dg.N = g->N;
+    c->dg.M = g->M;
+    c->dg.q = q;
+    c->dg.m = g->m;
+    c->dg.E = g->E;
+    c->dg.row_ptr = (const int32_t *)(base + o_rp);
+    c->dg.row_col = (const int32_t *)(base + o_rc);
+    c->dg.col_ptr = (const int32_t *)(base + o_cp);
+    c->dg.col_slot = (const int32_t *)(base + o_cs);
+    c->dg.row_h = base + o_h;
+    c->dg.gf_mul = base + o_mul;
+    c->dg.gf_inv = base + o_inv;
+    NB_HIP_TRY(c->counts.ensure(8 * sizeof(unsigned long long)));
+    NB_HIP_TRY(hipMemset(c->counts.p, 0, 8 * sizeof(unsigned long long)));
+    *out = c;
+    return LDPC_OK;
+}
+
+int ldpc_nb_ctx_set_stream(ldpc_nb_ctx *c, void *hip_stream)
+{
+    if (!c) return err(LDPC_ERR_INVALID, "ctx is null");
+    c->stream = hip_stream ? (hipStream_t)hip_stream : c->own;
+    return LDPC_OK;
+}
+
+void ldpc_nb_ctx_destroy(ldpc_nb_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->own);
+    for (Buf *b : {&c->graph, &c->counts, &c->y_stage, &c->c_stage, &c->d_stage, &c->fr_stage, &c->scratch})
+        b->release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+static int check_ems(const ldpc_nb_ctx *c, const ldpc_ems_cfg *cfg, int batch)
+{
+    if (!c || !cfg) return err(LDPC_ERR_INVALID, "null argument");
+    if (batch <= 0 || batch > c->max_batch)
+        return err(LDPC_ERR_INVALID, "batch %d outside 1..max_batch=%d", batch, c->max_batch);
+    if (cfg->T < 0) return err(LDPC_ERR_INVALID, "T must be >= 0");
+    if (cfg->nm < 1) return err(LDPC_ERR_INVALID, "nm must be >= 1");
+    if (!(cfg->offset >= 0)) return err(LDPC_ERR_INVALID, "offset must be >= 0");
+    return LDPC_OK;
+}
+
+static int read_counts_raw(ldpc_nb_ctx *c, unsigned long long *v)
+{
+    NB_HIP_TRY(hipMemcpyAsync(v, c->counts.p, 7 * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+    NB_HIP_TRY(hipStreamSynchronize(c->stream));
+    return LDPC_OK;
+}
+
+static void add_counts(ldpc_nb_counts *acc, const unsigned long long *after, const unsigned long long *before)
+{
+    acc->bit_err += (int64_t)(after[0] - before[0]);
+    acc->frame_err += (int64_t)(after[1] - before[1]);
+    acc->uncoded_bit_err += (int64_t)(after[2] - before[2]);
+    acc->frames += (int64_t)(after[3] - before[3]);
+    acc->iters += (int64_t)(after[4] - before[4]);
+    acc->syndrome_fail += (int64_t)(after[5] - before[5]);
+    acc->symbol_err += (int64_t)(after[6] - before[6]);
+}
+
+static int run(ldpc_nb_ctx *c, const ldpc::NbArgs &a)
+{
+    const ldpc::NbChoice ch = ldpc::nb_choose(c->dg, c->g->maxdc);
+    int slots = 0;
+    if (ch.slot_bytes) {
+        slots = std::min(a.batch, c->num_cus);
+        NB_HIP_TRY(c->scratch.ensure(ch.slot_bytes * (size_t)slots));
+    }
+    NB_HIP_TRY(hipEventRecord(c->ev0, c->stream));
+    NB_HIP_TRY(ldpc::nb_launch(c->dg, a, ch, c->scratch.p, slots, c->num_cus, c->stream));
+    NB_HIP_TRY(hipEventRecord(c->ev1, c->stream));
+    c->timed = true;
+    return LDPC_OK;
+}
+
+static void fill_cfg(ldpc::NbArgs &a, ldpc_nb_ctx *c, const ldpc_ems_cfg *cfg, int batch)
+{
+    std::memset(&a, 0, sizeof a);
+    a.batch = batch;
+    a.T = cfg->T;
+    a.nm = cfg->nm;
+    a.early_stop = cfg->early_stop ? 1 : 0;
+    a.offset = (float)cfg->offset;
+    a.counts = (unsigned long long *)c->counts.p;
+}
+
+int ldpc_ems_decode_batch(ldpc_nb_ctx *c, const float *y, int batch, double n0, const ldpc_ems_cfg *cfg,
+                          const uint8_t *cw, uint8_t *d_out, ldpc_frame_result *frames, ldpc_nb_counts *counts)
+{
+    int rc = check_ems(c, cfg, batch);
+    if (rc) return rc;
+    if (!y) return err(LDPC_ERR_INVALID, "y is null");
+    if (!(n0 > 0)) return err(LDPC_ERR_INVALID, "n0 must be > 0");
+    NB_HIP_TRY(hipSetDevice(c->device));
+    const int N = c->g->N, m = c->g->m;
+    ldpc::NbArgs a;
+    fill_cfg(a, c, cfg, batch);
+    a.src = ldpc::SRC_GIVEN;
+    a.n0 = (float)n0;
+    const size_t yb = (size_t)batch * N * m * sizeof(float), nb = (size_t)batch * N;
+    if (is_device_ptr(y)) {
+        a.y = y;
+    } else {
+        NB_HIP_TRY(c->y_stage.ensure(yb));
+        NB_HIP_TRY(hipMemcpyAsync(c->y_stage.p, y, yb, hipMemcpyHostToDevice, c->stream));
+        a.y = (const float *)c->y_stage.p;
+    }
+    if (cw) {
+        for (size_t i = 0; !is_device_ptr(cw) && i < nb; ++i)
+            if (cw[i] >= (unsigned)c->g->q) return err(LDPC_ERR_INVALID, "codeword symbol %zu is %d (q=%d)", i, cw[i], c->g->q);
+        if (is_device_ptr(cw)) {
+            a.c = cw;
+        } else {
+            NB_HIP_TRY(c->c_stage.ensure(nb));
+            NB_HIP_TRY(hipMemcpyAsync(c->c_stage.p, cw, nb, hipMemcpyHostToDevice, c->stream));
+            a.c = (const uint8_t *)c->c_stage.p;
+        }
+    }
+    const bool d_host = d_out && !is_device_ptr(d_out), f_host = frames && !is_device_ptr(frames);
+    if (d_host) {
+        NB_HIP_TRY(c->d_stage.ensure(nb));
+        a.d_out = (uint8_t *)c->d_stage.p;
+    } else {
+        a.d_out = d_out;
+    }
+    if (f_host) {
+        NB_HIP_TRY(c->fr_stage.ensure(sizeof(ldpc_frame_result) * (size_t)batch));
+        a.frame_res = (int4 *)c->fr_stage.p;
+    } else {
+        a.frame_res = (int4 *)frames;
+    }
+    unsigned long long before[7], after[7];
+    rc = read_counts_raw(c, before);
+    if (rc) return rc;
+    rc = run(c, a);
+    if (rc) return rc;
+    if (d_host) NB_HIP_TRY(hipMemcpyAsync(d_out, c->d_stage.p, nb, hipMemcpyDeviceToHost, c->stream));
+    if (f_host)
+        NB_HIP_TRY(hipMemcpyAsync(frames, c->fr_stage.p, sizeof(ldpc_frame_result) * (size_t)batch,
+                                  hipMemcpyDeviceToHost, c->stream));
+    rc = read_counts_raw(c, after);
+    if (rc) return rc;
+    if (counts) add_counts(counts, after, before);
+    return LDPC_OK;
+}
+
+static int sim_impl(ldpc_nb_ctx *c, double ebn0_db, double R, const ldpc_ems_cfg *cfg, uint64_t seed,
+                    uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames_dev, float *y_dev,
+                    uint8_t *d_dev)
+{
+    int rc = check_ems(c, cfg, batch);
+    if (rc) return rc;
+    if (!(R > 0)) return err(LDPC_ERR_INVALID, "rate must be > 0");
+    NB_HIP_TRY(hipSetDevice(c->device));
+    ldpc::NbArgs a;
+    fill_cfg(a, c, cfg, batch);
+    a.src = ldpc::SRC_PHILOX;
+    const double N0 = std::pow(10.0, -ebn0_db / 10.0) / R;   // decodeMinSum.cpp:146-147
+    a.n0 = (float)N0;
+    a.sigma = (float)std::sqrt(N0 / 2.0);
+    a.seed = seed;
+    a.stream_id = stream_id;
+    a.first_cw = first_cw;
+    a.frame_res = (int4 *)frames_dev;
+    a.y_out = y_dev;
+    a.d_out = d_dev;
+    return run(c, a);
+}
+
+int ldpc_ems_sim_launch(ldpc_nb_ctx *c, double ebn0_db, double R, const ldpc_ems_cfg *cfg, uint64_t seed,
+                        uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames_dev)
+{
+    if (frames_dev && !is_device_ptr(frames_dev)) return err(LDPC_ERR_INVALID, "frames_dev must be device memory");
+    return sim_impl(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, frames_dev, nullptr, nullptr);
+}
+
+int ldpc_ems_sim_trace(ldpc_nb_ctx *c, double ebn0_db, double R, const ldpc_ems_cfg *cfg, uint64_t seed,
+                       uint32_t stream_id, uint64_t first_cw, int batch, float *y_out, uint8_t *d_out,
+                       ldpc_frame_result *frames, ldpc_nb_counts *accum)
+{
+    int rc = check_ems(c, cfg, batch);
+    if (rc) return rc;
+    const int N = c->g->N, m = c->g->m;
+    const size_t yb = (size_t)batch * N * m * sizeof(float), nb = (size_t)batch * N;
+    const bool y_host = y_out && !is_device_ptr(y_out), d_host = d_out && !is_device_ptr(d_out),
+               f_host = frames && !is_device_ptr(frames);
+    float *yd = y_out;
+    uint8_t *dd = d_out;
+    ldpc_frame_result *fd = frames;
+    if (y_host) {
+        NB_HIP_TRY(c->y_stage.ensure(yb));
+        yd = (float *)c->y_stage.p;
+    }
+    if (d_host) {
+        NB_HIP_TRY(c->d_stage.ensure(nb));
+        dd = (uint8_t *)c->d_stage.p;
+    }
+    if (f_host) {
+        NB_HIP_TRY(c->fr_stage.ensure(sizeof(ldpc_frame_result) * (size_t)batch));
+        fd = (ldpc_frame_result *)c->fr_stage.p;
+    }
+    unsigned long long before[7], after[7];
+    rc = read_counts_raw(c, before);
+    if (rc) return rc;
+    rc = sim_impl(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, fd, yd, dd);
+    if (rc) return rc;
+    if (y_host) NB_HIP_TRY(hipMemcpyAsync(y_out, yd, yb, hipMemcpyDeviceToHost, c->stream));
+    if (d_host) NB_HIP_TRY(hipMemcpyAsync(d_out, dd, nb, hipMemcpyDeviceToHost, c->stream));
+    if (f_host)
+        NB_HIP_TRY(hipMemcpyAsync(frames, fd, sizeof(ldpc_frame_result) * (size_t)batch, hipMemcpyDeviceToHost,
+                                  c->stream));
+    rc = read_counts_raw(c, after);
+    if (rc) return rc;
+    if (accum) add_counts(accum, after, before);
+    return LDPC_OK;
+}
+
+int ldpc_ems_sim_batch(ldpc_nb_ctx *c, double ebn0_db, double R, const ldpc_ems_cfg *cfg, uint64_t seed,
+                       uint32_t stream_id, uint64_t first_cw, int batch, ldpc_frame_result *frames,
+                       ldpc_nb_counts *accum)
+{
+    return ldpc_ems_sim_trace(c, ebn0_db, R, cfg, seed, stream_id, first_cw, batch, nullptr, nullptr, frames, accum);
+}
+
+int ldpc_nb_ctx_read_counts(ldpc_nb_ctx *c, ldpc_nb_counts *out, int reset)
+{
+    if (!c || !out) return err(LDPC_ERR_INVALID, "null argument");
+    NB_HIP_TRY(hipSetDevice(c->device));
+    unsigned long long v[7], z[7] = {0, 0, 0, 0, 0, 0, 0};
+    int rc = read_counts_raw(c, v);
+    if (rc) return rc;
+    std::memset(out, 0, sizeof *out);
+    add_counts(out, v, z);
+    if (reset) {
+        NB_HIP_TRY(hipMemsetAsync(c->counts.p, 0, 7 * sizeof(unsigned long long), c->stream));
+        NB_HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return LDPC_OK;
+}
+
+int ldpc_nb_ctx_last_kernel_ms(ldpc_nb_ctx *c, float *ms)
+{
+    if (!c || !ms) return err(LDPC_ERR_INVALID, "null argument");
+    if (!c->timed) return err(LDPC_ERR_INVALID, "no kernel launched yet");
+    NB_HIP_TRY(hipEventSynchronize(c->ev1));
+    NB_HIP_TRY(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return LDPC_OK;
+}
+
+int ldpc_ems_kernel_info(ldpc_nb_ctx *c, char *name, int name_len, int *lds_bytes)
+{
+    if (!c) return err(LDPC_ERR_INVALID, "ctx is null");
+    const ldpc::NbChoice ch = ldpc::nb_choose(c->dg, c->g->maxdc);
+    if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", ch.name);
+    if (lds_bytes) *lds_bytes = ch.lds_bytes;
+    return LDPC_OK;
+}
+
+}  // extern "C"

@@ -22,7 +22,7 @@ LDPC_OK = 0
 MS, NMS, OMS, BP = 0, 1, 2, 3
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
@@ -111,6 +111,31 @@ class DecoderConfig:
                     self.qbits, self.ymax, self.alpha, self.delta, self.schedule, 0, self.n0, self.max_llr)
 
 
+class _EmsCfg(C.Structure):
+    _fields_ = [("T", C.c_int32), ("nm", C.c_int32), ("early_stop", C.c_int32), ("reserved", C.c_int32),
+                ("offset", C.c_double)]
+
+
+class NbCounts(C.Structure):
+    _fields_ = [(k, C.c_int64) for k in ("bit_err", "frame_err", "uncoded_bit_err", "frames", "iters",
+                                         "syndrome_fail", "symbol_err")]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+@dataclass
+class EmsConfig:
+    """Extended Min-Sum over GF(q) (include/ldpc_hip.h ldpc_ems_cfg)."""
+    T: int = 20
+    nm: int = 16                 # message truncation (>= q: full vectors)
+    offset: float = 0.0          # fill offset for truncated symbols
+    early_stop: bool = True      # stop when H d = 0
+
+    def _c(self) -> _EmsCfg:
+        return _EmsCfg(self.T, self.nm, int(self.early_stop), 0, self.offset)
+
+
 _lib = None
 
 
@@ -151,6 +176,22 @@ def lib():
         "ldpc_gdbf_sim_batch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp, C.POINTER(Counts)],
                                 i32),
         "ldpc_gdbf_kernel_info": ([vp, C.POINTER(_GdbfCfg), C.c_char_p, i32, C.POINTER(i32)], i32),
+        "ldpc_nb_graph_create": ([i32, i32, i32, vp, vp, vp, vp, vp, vp, C.POINTER(vp)], i32),
+        "ldpc_nb_graph_load_alist": ([C.c_char_p, C.POINTER(vp)], i32),
+        "ldpc_nb_graph_info": ([vp] + [C.POINTER(i32)] * 6, i32),
+        "ldpc_nb_graph_destroy": ([vp], None),
+        "ldpc_nb_ctx_create": ([i32, vp, i32, C.POINTER(vp)], i32),
+        "ldpc_nb_ctx_set_stream": ([vp, vp], i32),
+        "ldpc_nb_ctx_destroy": ([vp], None),
+        "ldpc_nb_ctx_read_counts": ([vp, C.POINTER(NbCounts), i32], i32),
+        "ldpc_nb_ctx_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i32),
+        "ldpc_ems_kernel_info": ([vp, C.c_char_p, i32, C.POINTER(i32)], i32),
+        "ldpc_ems_decode_batch": ([vp, vp, i32, dbl, C.POINTER(_EmsCfg), vp, vp, vp, C.POINTER(NbCounts)], i32),
+        "ldpc_ems_sim_launch": ([vp, dbl, dbl, C.POINTER(_EmsCfg), u64, u32, u64, i32, vp], i32),
+        "ldpc_ems_sim_batch": ([vp, dbl, dbl, C.POINTER(_EmsCfg), u64, u32, u64, i32, vp, C.POINTER(NbCounts)],
+                               i32),
+        "ldpc_ems_sim_trace": ([vp, dbl, dbl, C.POINTER(_EmsCfg), u64, u32, u64, i32, vp, vp, vp,
+                                C.POINTER(NbCounts)], i32),
     }
     for name, (argt, rest) in sig.items():
         fn = getattr(L, name)
@@ -168,7 +209,11 @@ EXPORTED = ["ldpc_abi_version", "ldpc_last_error", "ldpc_graph_create", "ldpc_gr
             "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
             "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",
             "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info",
-            "ldpc_gdbf_decode_batch", "ldpc_gdbf_sim_launch", "ldpc_gdbf_sim_batch", "ldpc_gdbf_kernel_info"]
+            "ldpc_gdbf_decode_batch", "ldpc_gdbf_sim_launch", "ldpc_gdbf_sim_batch", "ldpc_gdbf_kernel_info",
+            "ldpc_nb_graph_create", "ldpc_nb_graph_load_alist", "ldpc_nb_graph_info", "ldpc_nb_graph_destroy",
+            "ldpc_nb_ctx_create", "ldpc_nb_ctx_set_stream", "ldpc_nb_ctx_destroy", "ldpc_nb_ctx_read_counts",
+            "ldpc_nb_ctx_last_kernel_ms", "ldpc_ems_kernel_info", "ldpc_ems_decode_batch", "ldpc_ems_sim_launch",
+            "ldpc_ems_sim_batch", "ldpc_ems_sim_trace"]
 
 
 def _check(rc: int):
@@ -374,4 +419,124 @@ class Context:
         name = C.create_string_buffer(32)
         lds = C.c_int()
         _check(lib().ldpc_gdbf_kernel_info(self._h, C.byref(cfg._c()), name, 32, C.byref(lds)))
+        return {"kernel": name.value.decode(), "lds_bytes": lds.value}
+
+
+# ---- non-binary GF(q) codes, Extended Min-Sum (BASELINE config 5) ----
+class NbGraph:
+    """GF(q) Tanner graph (NB alist of SystemC/NB-LDPC/src/alist.cpp)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        N, M, q, E, dv, dc = (C.c_int() for _ in range(6))
+        _check(lib().ldpc_nb_graph_info(handle, C.byref(N), C.byref(M), C.byref(q), C.byref(E), C.byref(dv),
+                                        C.byref(dc)))
+        self.N, self.M, self.q, self.E, self.maxdv, self.maxdc = N.value, M.value, q.value, E.value, dv.value, dc.value
+        self.m = self.q.bit_length() - 1
+
+    @classmethod
+    def from_alist(cls, path: str) -> "NbGraph":
+        h = C.c_void_p()
+        _check(lib().ldpc_nb_graph_load_alist(path.encode(), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def from_lists(cls, N: int, M: int, q: int, cols, rows) -> "NbGraph":
+        """cols[i] = [(row, h), ...], rows[j] = [(col, h), ...], 0-based (as codes.NbParityCheck)."""
+        def arrs(lists, one_based):
+            n = (C.c_int * len(lists))(*[len(l) for l in lists])
+            idx = [(C.c_int * max(len(l), 1))(*[a + 1 for a, _ in l]) for l in lists]
+            val = [(C.c_int * max(len(l), 1))(*[h for _, h in l]) for l in lists]
+            pi = (C.POINTER(C.c_int) * len(lists))(*[C.cast(a, C.POINTER(C.c_int)) for a in idx])
+            pv = (C.POINTER(C.c_int) * len(lists))(*[C.cast(a, C.POINTER(C.c_int)) for a in val])
+            return n, pi, pv, (idx, val)
+        nn, ni, nv, keep1 = arrs(cols, True)
+        mn, mi, mv, keep2 = arrs(rows, True)
+        h = C.c_void_p()
+        _check(lib().ldpc_nb_graph_create(N, M, q, nn, ni, nv, mn, mi, mv, C.byref(h)))
+        return cls(h)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.ldpc_nb_graph_destroy(h)
+            self._h = None
+
+
+class NbContext:
+    """Device context of the EMS decoder (GF(16))."""
+
+    def __init__(self, graph: NbGraph, device: int = 0, max_batch: int = 65536):
+        self.graph = graph
+        self.max_batch = max_batch
+        h = C.c_void_p()
+        _check(lib().ldpc_nb_ctx_create(device, graph._h, max_batch, C.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.ldpc_nb_ctx_destroy(h)
+            self._h = None
+
+    def set_stream(self, stream_handle: Optional[int]):
+        _check(lib().ldpc_nb_ctx_set_stream(self._h, stream_handle))
+
+    def decode(self, y, n0: float, cfg: EmsConfig, c=None, want_decisions: bool = True):
+        """Decode y[batch, N*m] float32 (numpy or torch, host or device). Returns (d [batch,N] uint8, frames, NbCounts)."""
+        g = self.graph
+        if isinstance(y, np.ndarray):
+            if y.dtype != np.float32:
+                raise TypeError(f"y must be float32, got {y.dtype}")
+            y = np.ascontiguousarray(y)
+            batch = y.size // (g.N * g.m)
+        else:
+            batch = y.numel() // (g.N * g.m)
+        if c is not None and isinstance(c, np.ndarray):
+            c = np.ascontiguousarray(c, dtype=np.uint8)
+        d = np.empty((batch, g.N), dtype=np.uint8) if want_decisions else None
+        fr = np.empty(batch, dtype=FRAME_DTYPE)
+        cnt = NbCounts()
+        _check(lib().ldpc_ems_decode_batch(self._h, _ptr(y), batch, n0, C.byref(cfg._c()), _ptr(c), _ptr(d),
+                                           _ptr(fr), C.byref(cnt)))
+        return d, fr, cnt
+
+    def sim_launch(self, ebn0_db: float, R: float, cfg: EmsConfig, seed: int, stream_id: int, first_cw: int,
+                   batch: int, frames_dev=None):
+        _check(lib().ldpc_ems_sim_launch(self._h, ebn0_db, R, C.byref(cfg._c()), seed, stream_id, first_cw, batch,
+                                         _ptr(frames_dev)))
+
+    def sim_batch(self, ebn0_db: float, R: float, cfg: EmsConfig, seed: int, stream_id: int, first_cw: int,
+                  batch: int):
+        fr = np.empty(batch, dtype=FRAME_DTYPE)
+        cnt = NbCounts()
+        _check(lib().ldpc_ems_sim_batch(self._h, ebn0_db, R, C.byref(cfg._c()), seed, stream_id, first_cw, batch,
+                                        fr.ctypes.data, C.byref(cnt)))
+        return fr, cnt
+
+    def sim_trace(self, ebn0_db: float, R: float, cfg: EmsConfig, seed: int, stream_id: int, first_cw: int,
+                  batch: int):
+        g = self.graph
+        y = np.empty((batch, g.N * g.m), dtype=np.float32)
+        d = np.empty((batch, g.N), dtype=np.uint8)
+        fr = np.empty(batch, dtype=FRAME_DTYPE)
+        cnt = NbCounts()
+        _check(lib().ldpc_ems_sim_trace(self._h, ebn0_db, R, C.byref(cfg._c()), seed, stream_id, first_cw, batch,
+                                        y.ctypes.data, d.ctypes.data, fr.ctypes.data, C.byref(cnt)))
+        return y, d, fr, cnt
+
+    def read_counts(self, reset: bool = False) -> NbCounts:
+        cnt = NbCounts()
+        _check(lib().ldpc_nb_ctx_read_counts(self._h, C.byref(cnt), int(reset)))
+        return cnt
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        _check(lib().ldpc_nb_ctx_last_kernel_ms(self._h, C.byref(ms)))
+        return float(ms.value)
+
+    def kernel_info(self) -> dict:
+        name = C.create_string_buffer(32)
+        lds = C.c_int()
+        _check(lib().ldpc_ems_kernel_info(self._h, name, 32, C.byref(lds)))
         return {"kernel": name.value.decode(), "lds_bytes": lds.value}

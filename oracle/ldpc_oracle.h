@@ -149,6 +149,14 @@ int64_t orc_bp_run(const orc_alist *H, double R, double snr, int T, uint32_t see
                    const char *const *cw_lines, int ncw, int64_t max_frames,
                    int32_t *frame_w, int64_t cap, orc_stats *out);
 
+/* ---- non-binary GF(q) EMS (ems_oracle.c; parity unpinned, see there) ---- */
+int  orc_gf_poly(int q);
+int  orc_gf_mul(int q, int a, int b);
+void orc_nb_front(const float *y, int n, float n0, float *lam);
+int  orc_ems_decode(int N, int M, int q, const int *row_ptr, const int *row_col, const int *row_h,
+                    const int *col_ptr, const int *col_slot, const float *lam, int T, int nm, float offset,
+                    int early_stop, uint8_t *d, int *synd_fail);
+
 /* Philox4x32-10 (Random123 reference constants). */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 

@@ -322,3 +322,46 @@ def philox4x32_10(ctr, key) -> list:
     o = np.empty(4, dtype=np.uint32)
     lib().orc_philox4x32_10(c.ctypes.data, k.ctypes.data, o.ctypes.data)
     return [int(x) for x in o]
+
+
+class NbCode:
+    """GF(q) code (ldpcsimulation_amd.codes.NbParityCheck) bound to the EMS oracle (ems_oracle.c)."""
+
+    def __init__(self, H):
+        self.H = H
+        self.N, self.M, self.q = H.N, H.M, H.q
+        self.m = q_bits = int(H.q).bit_length() - 1
+        assert 1 << q_bits == H.q
+        self._csr = [np.ascontiguousarray(a, dtype=np.int32) for a in H.csr()]
+        L = lib()
+        if not getattr(L, "_ems_set", False):
+            L.orc_gf_mul.argtypes = [C.c_int, C.c_int, C.c_int]
+            L.orc_gf_mul.restype = C.c_int
+            L.orc_nb_front.argtypes = [C.c_void_p, C.c_int, C.c_float, C.c_void_p]
+            L.orc_ems_decode.argtypes = [C.c_int, C.c_int, C.c_int] + [C.c_void_p] * 6 + [
+                C.c_int, C.c_int, C.c_float, C.c_int, C.c_void_p, C.POINTER(C.c_int)]
+            L.orc_ems_decode.restype = C.c_int
+            L._ems_set = True
+
+    def front(self, y: np.ndarray, n0: float) -> np.ndarray:
+        y = np.ascontiguousarray(y, dtype=np.float32)
+        lam = np.empty_like(y)
+        lib().orc_nb_front(y.ctypes.data, y.size, n0, lam.ctypes.data)
+        return lam
+
+    def decode(self, y: np.ndarray, n0: float, T: int, nm: int = 16, offset: float = 0.0, early_stop: bool = True):
+        """EMS decode of y[B, N*m] (fp32 channel samples). Returns (d [B,N] uint8, iters [B], syndrome_fail [B])."""
+        y2 = np.ascontiguousarray(y, dtype=np.float32).reshape(-1, self.N * self.m)
+        B = y2.shape[0]
+        d = np.empty((B, self.N), dtype=np.uint8)
+        its = np.empty(B, dtype=np.int32)
+        sf = np.empty(B, dtype=np.int32)
+        rp, rc, rh, cp, cs = self._csr
+        for b in range(B):
+            lam = self.front(y2[b], n0)
+            f = C.c_int()
+            its[b] = lib().orc_ems_decode(self.N, self.M, self.q, rp.ctypes.data, rc.ctypes.data, rh.ctypes.data,
+                                          cp.ctypes.data, cs.ctypes.data, lam.ctypes.data, T, nm, offset,
+                                          int(early_stop), d[b].ctypes.data, C.byref(f))
+            sf[b] = f.value
+        return d, its, sf

@@ -1,0 +1,233 @@
+"""Non-binary GF(16) Extended Min-Sum (BASELINE config 5).
+
+PARITY UNPINNED against the reference: its NB-LDPC model
+(SystemC/NB-LDPC/inc/nodes.h) is a q^dc-LUT BP that does not compile, holds
+no EMS and no GF(16) code. The oracle (oracle/ems_oracle.c) restates the EMS
+of Declercq & Fossorier (2007) as DESIGN.md §11 defines it, and is anchored
+where the reference does pin something:
+  - the NB alist format of SystemC/NB-LDPC/src/alist.cpp:23-56 (round trip,
+    validation);
+  - q = 2: GF(2) EMS is binary min-sum, so the EMS oracle must give exactly
+    the decisions of the min-sum oracle, which reproduces the reference's
+    decodeMinSum runs frame by frame (tests/test_oracle.py).
+GPU tier: the HIP kernel (nb.hip) against the oracle, bit for bit: same
+decided symbols, iteration counts, syndrome flags and error counts.
+"""
+import hashlib
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import code_path
+from oracle import oracle as O
+
+GF16 = "gf16_N1000_dv2_dc4.alist"
+GF16_MD5 = "2e1fc43f5e523c3b86fbe09a64aefb40"
+
+
+def _codes():
+    from ldpcsimulation_amd import codes
+    return codes
+
+
+def _frames(nb, nframes, ebn0, seed, R=0.5, c=None):
+    """BPSK per bit (bit i of the symbol value, 0 -> +1), y = x(1 + sigma n), float32."""
+    rng = np.random.default_rng(seed)
+    n0 = 10 ** (-ebn0 / 10) / R
+    sigma = math.sqrt(n0 / 2)
+    x = np.ones((nframes, nb), dtype=np.float64)
+    if c is not None:
+        bits = (c[:, :, None] >> np.arange(4)) & 1
+        x = 1.0 - 2.0 * bits.reshape(nframes, nb)
+    y = (x * (1 + sigma * rng.standard_normal((nframes, nb)))).astype(np.float32)
+    return y, n0
+
+
+# ------------------------------------------------------------------ CPU tier
+def test_gf16_field_axioms():
+    codes = _codes()
+    q = 16
+    mul = np.array([[codes.gf_mul(q, a, b) for b in range(q)] for a in range(q)])
+    L = O.lib()
+    O.NbCode(codes.read_nb_alist(code_path(GF16)))     # sets the oracle signatures
+    assert all(L.orc_gf_mul(q, a, b) == mul[a, b] for a in range(q) for b in range(q))
+    assert (mul == mul.T).all() and (mul[1] == np.arange(q)).all() and (mul[0] == 0).all()
+    for a in range(1, q):
+        assert sorted(mul[a, 1:]) == list(range(1, q))          # nonzero row is a permutation
+    for a in range(q):
+        for b in range(q):
+            for c in range(q):
+                assert mul[mul[a, b], c] == mul[a, mul[b, c]]
+                assert mul[a, b ^ c] == mul[a, b] ^ mul[a, c]
+    # x^4 + x + 1 is primitive: alpha = 2 has order 15
+    p, order = 1, 0
+    while True:
+        p, order = mul[p, 2], order + 1
+        if p == 1:
+            break
+    assert order == 15
+
+
+def test_gf16_code_fixture_pinned_and_regular():
+    codes = _codes()
+    path = code_path(GF16)
+    assert hashlib.md5(open(path, "rb").read()).hexdigest() == GF16_MD5
+    H = codes.read_nb_alist(path)
+    assert (H.N, H.M, H.q, H.E) == (1000, 500, 16, 2000)
+    assert {len(r) for r in H.rows} == {4} and {len(c) for c in H.cols} == {2}
+    assert codes.nb_girth_at_least_6(H)
+    assert codes.nb_alist_text(H) == open(path).read()
+    # the generator reproduces the fixture
+    assert codes.nb_alist_text(codes.peg_nb_code(1000, 500, 2, 16, seed=16)) == open(path).read()
+
+
+def test_nb_alist_loader_rejects_inconsistent_views(tmp_path):
+    codes = _codes()
+    H = codes.read_nb_alist(code_path(GF16))
+    txt = codes.nb_alist_text(H).splitlines()
+    head = 4
+    row0 = txt[head + H.N].split()
+    row0[1] = str(int(row0[1]) % 15 + 1)                 # change one coefficient in the row view
+    txt[head + H.N] = " ".join(row0)
+    p = tmp_path / "bad.alist"
+    p.write_text("\n".join(txt) + "\n")
+    with pytest.raises(ValueError):
+        codes.read_nb_alist(str(p))
+    from ldpcsimulation_amd import native
+    with pytest.raises(native.LdpcError) as e:
+        native.NbGraph.from_alist(str(p))
+    assert e.value.code == -6
+    g = native.NbGraph.from_alist(code_path(GF16))
+    assert (g.N, g.M, g.q, g.E, g.maxdv, g.maxdc) == (1000, 500, 16, 2000, 2, 4)
+
+
+def test_ems_q2_equals_binary_min_sum_oracle():
+    """GF(2) EMS (nm = 2, no offset, no early stop) is binary min-sum: identical decisions to the
+    reference-pinned min-sum oracle on the same bit LLRs (PEGReg504x1008, glibc noise)."""
+    codes = _codes()
+    P = codes.read_alist(code_path("PEGReg504x1008.alist"))
+    H = codes.NbParityCheck(P.N, P.M, 2, [[(i, 1) for i in r] for r in P.rows], [[(j, 1) for j in c] for c in P.cols])
+    A, B = O.NbCode(H), O.Alist(code_path("PEGReg504x1008.alist"))
+    n0 = 10 ** (-2.0 / 10) / 0.5
+    g = O.GlibcRandom(5)
+    y = np.stack([g.channel(np.ones(P.N, dtype=np.int32), math.sqrt(n0 / 2)) for _ in range(30)]).astype(np.float32)
+    lam = np.stack([A.front(r, n0) for r in y]).astype(np.float64)
+    for T in (1, 5, 10):
+        d, its, _ = A.decode(y, n0, T, nm=2, early_stop=False)
+        want = (B.decode(lam, T, O.Cfg()) == -1).astype(np.uint8)
+        assert np.array_equal(d, want), f"T={T}"
+        assert (its == T).all()
+
+
+def test_ems_oracle_properties():
+    codes = _codes()
+    H = codes.read_nb_alist(code_path(GF16))
+    A = O.NbCode(H)
+    y, n0 = _frames(H.N * 4, 6, 1.8, seed=3)
+    lam = np.stack([A.front(r, n0) for r in y])
+    hard = ((lam.reshape(6, H.N, 4) < 0) << np.arange(4)).sum(axis=2)
+    d0, its0, _ = A.decode(y, n0, 0)
+    assert np.array_equal(d0, hard) and (its0 == 0).all()       # T = 0: the channel's hard decisions
+    d, its, sf = A.decode(y, n0, 30, nm=16, early_stop=True)
+    for b in range(6):
+        synd = H.syndrome(d[b])
+        assert (sf[b] == 0) == (not any(synd))
+        if its[b] < 30:
+            assert sf[b] == 0                                    # early stop only on a codeword
+    # a high-SNR frame decodes within a couple of iterations
+    yc, n0c = _frames(H.N * 4, 1, 8.0, seed=4)
+    dc, itc, sfc = A.decode(yc, n0c, 10)
+    assert (dc == 0).all() and itc[0] <= 2 and sfc[0] == 0
+
+
+# ------------------------------------------------------------------ GPU tier
+def _native():
+    from ldpcsimulation_amd import native
+    return native
+
+
+@pytest.fixture(scope="module")
+def nbctx():
+    native = _native()
+    g = native.NbGraph.from_alist(code_path(GF16))
+    return native.NbContext(g, 0, 4096)
+
+
+EMS_CFGS = [dict(nm=16, offset=0.0, early_stop=True), dict(nm=16, offset=0.0, early_stop=False),
+            dict(nm=8, offset=0.5, early_stop=True), dict(nm=4, offset=1.0, early_stop=False),
+            dict(nm=12, offset=0.25, early_stop=True)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ci", range(len(EMS_CFGS)))
+def test_ems_decisions_bit_exact_vs_oracle(nbctx, ci):
+    native = _native()
+    c = EMS_CFGS[ci]
+    H = _codes().read_nb_alist(code_path(GF16))
+    A = O.NbCode(H)
+    y, n0 = _frames(H.N * 4, 8, 1.6, seed=100 + ci)
+    for T in (0, 1, 3, 15):
+        d, fr, cnt = nbctx.decode(y, n0, native.EmsConfig(T=T, **c))
+        want, its, sf = A.decode(y, n0, T, **c)
+        assert int((d != want).sum()) == 0, f"T={T}: {(d != want).sum()} symbols differ"
+        assert np.array_equal(fr["iters"], its) and np.array_equal(fr["syndrome_fail"], sf)
+        be = np.array([sum(bin(int(s)).count("1") for s in row) for row in want])
+        assert np.array_equal(fr["bit_err"], be)
+        assert cnt.frames == 8 and cnt.iters == int(its.sum()) and cnt.bit_err == int(be.sum())
+        assert cnt.symbol_err == int((want != 0).sum()) and cnt.frame_err == int((want != 0).any(axis=1).sum())
+
+
+@pytest.mark.gpu
+def test_ems_given_codeword_accounting(nbctx):
+    native = _native()
+    H = _codes().read_nb_alist(code_path(GF16))
+    A = O.NbCode(H)
+    rng = np.random.default_rng(9)
+    c = rng.integers(0, 16, size=(4, H.N), dtype=np.uint8)      # accounting only: any symbols
+    y, n0 = _frames(H.N * 4, 4, 2.0, seed=11, c=c)
+    d, fr, cnt = nbctx.decode(y, n0, native.EmsConfig(T=5), c=c)
+    want, _, _ = A.decode(y, n0, 5)
+    assert np.array_equal(d, want)
+    be = np.array([sum(bin(int(a) ^ int(b)).count("1") for a, b in zip(dr, cr)) for dr, cr in zip(want, c)])
+    assert np.array_equal(fr["bit_err"], be)
+    lam = np.stack([A.front(r, n0) for r in y]).reshape(4, H.N, 4)
+    unc = ((lam < 0) != ((c[:, :, None] >> np.arange(4)) & 1)).sum(axis=(1, 2))
+    assert np.array_equal(fr["uncoded_bit_err"], unc)
+
+
+@pytest.mark.gpu
+def test_ems_sim_on_device_noise_matches_oracle(nbctx):
+    native = _native()
+    H = _codes().read_nb_alist(code_path(GF16))
+    A = O.NbCode(H)
+    cfg = native.EmsConfig(T=20, nm=16)
+    y, d, fr, cnt = nbctx.sim_trace(1.5, 0.5, cfg, seed=7, stream_id=1, first_cw=300, batch=16)
+    n0 = 10 ** (-1.5 / 10) / 0.5
+    want, its, sf = A.decode(y, n0, 20)
+    assert np.array_equal(d, want) and np.array_equal(fr["iters"], its)
+    assert abs(float(y.mean()) - 1.0) < 0.02 and abs(float(y.std()) - math.sqrt(n0 / 2)) < 0.02
+
+
+@pytest.mark.gpu
+def test_ems_sim_independent_of_batch_split(nbctx):
+    native = _native()
+    cfg = native.EmsConfig(T=10)
+    full, _ = nbctx.sim_batch(1.5, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=300)
+    a, _ = nbctx.sim_batch(1.5, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=100)
+    b, _ = nbctx.sim_batch(1.5, 0.5, cfg, seed=5, stream_id=0, first_cw=100, batch=200)
+    assert np.array_equal(full, np.concatenate([a, b]))
+
+
+@pytest.mark.gpu
+def test_ems_waterfall(nbctx):
+    """FER falls with Eb/N0, early-stopped frames are codewords (parity unpinned: no reference FER)."""
+    native = _native()
+    cfg = native.EmsConfig(T=30, nm=16)
+    fer = []
+    for ebn0 in (1.0, 1.5, 2.0):
+        fr, cnt = nbctx.sim_batch(ebn0, 0.5, cfg, seed=13, stream_id=2, first_cw=0, batch=4096)
+        assert ((fr["iters"] < 30) <= (fr["syndrome_fail"] == 0)).all()
+        fer.append(cnt.frame_err / cnt.frames)
+    assert fer[0] > fer[1] > fer[2] and fer[0] > 0.5 and fer[2] < 0.05, fer
