@@ -138,21 +138,36 @@ __device__ __forceinline__ float sym_llr(const float *lam, int x)
     return s;
 }
 
-template <int Q, int MB>
-__device__ __forceinline__ int syndrome_fail(const NbDevGraph &g, const uint8_t *dec, const uint8_t *gmul)
+// The graph, re-packed into LDS once per workgroup (global loads in the
+// per-iteration loops would put two dependent HBM/L2 round trips on every
+// check and symbol round).
+struct NbSched {
+    const uint32_t *cn;      // [M]  r0 | d << 24
+    const uint8_t *ehinv;    // [E]  h^-1 of each edge slot
+    const uint8_t *eh;       // [E]  h
+    const uint16_t *ecol;    // [E]  symbol of each edge slot
+    const uint32_t *vn;      // [N]  first col entry << 8 | degree
+    const uint16_t *vslot;   // [E]  edge slots of each symbol, nlist order
+};
+
+template <int Q>
+__device__ __forceinline__ int syndrome_fail(const NbDevGraph &g, const NbSched &s, const uint8_t *dec,
+                                             const uint8_t *gmul)
 {
     int fail = 0;
     for (int j = threadIdx.x; j < g.M; j += blockDim.x) {
-        int s = 0;
-        for (int e = g.row_ptr[j]; e < g.row_ptr[j + 1]; ++e) s ^= gmul[g.row_h[e] * Q + dec[g.row_col[e]]];
-        fail |= s != 0;
+        const uint32_t sc = s.cn[j];
+        const int r0 = sc & 0xFFFFFF, d = sc >> 24;
+        int sy = 0;
+        for (int e = r0; e < r0 + d; ++e) sy ^= gmul[s.eh[e] * Q + dec[s.ecol[e]]];
+        fail |= sy != 0;
     }
     return __syncthreads_or(fail);
 }
 
 template <int Q, int MB, int DC, int SRC>
 __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &g, int b, float *msg, float *lam,
-                                             uint8_t *dec, const uint8_t *gmul, const uint8_t *ginv, int *red)
+                                             uint8_t *dec, const uint8_t *gmul, const NbSched &sc, int *red)
 {
     const int tid = threadIdx.x, nt = blockDim.x;
     const int x = tid & (Q - 1), grp = tid / Q, ngrp = nt / Q;
@@ -196,24 +211,26 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     // ---- initial messages v2c = L, decisions argmin L ----
     for (int v = grp; v < N; v += ngrp) {
         const float L = sym_llr<MB>(lam + v * MB, x);
-        for (int e = g.col_ptr[v]; e < g.col_ptr[v + 1]; ++e) msg[(size_t)g.col_slot[e] * Q + x] = L;
+        const uint32_t vp = sc.vn[v];
+        const int e0 = vp >> 8, e1 = e0 + (vp & 255);
+        for (int e = e0; e < e1; ++e) msg[(size_t)sc.vslot[e] * Q + x] = L;
         const int d = group_argmin<Q>(L, x);
         if (x == 0) dec[v] = (uint8_t)d;
     }
     __syncthreads();
-    int fail = syndrome_fail<Q, MB>(g, dec, gmul);
+    int fail = syndrome_fail<Q>(g, sc, dec, gmul);
     int it = 0;
     while (it < a.T && (!a.early_stop || fail)) {
         // ---- check nodes: forward-backward EMS ----
         for (int j = grp; j < M; j += ngrp) {
-            const int r0 = g.row_ptr[j], d = g.row_ptr[j + 1] - r0;
+            const uint32_t cs = sc.cn[j];
+            const int r0 = cs & 0xFFFFFF, d = cs >> 24;
             float U[DC], F[DC], B[DC];
             int idx[DC];
 #pragma unroll
             for (int k = 0; k < DC; ++k)
                 if (k < d) {
-                    const int h = g.row_h[r0 + k];
-                    idx[k] = (r0 + k) * Q + gmul[ginv[h] * Q + x];   // U(x) = v2c(h^-1 x)
+                    idx[k] = (r0 + k) * Q + gmul[sc.ehinv[r0 + k] * Q + x];   // U(x) = v2c(h^-1 x)
                     U[k] = trunc_nm<Q>(msg[idx[k]], x, a.nm);
                 }
             F[0] = U[0];
@@ -245,18 +262,19 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         // ---- symbol nodes ----
         for (int v = grp; v < N; v += ngrp) {
             float app = sym_llr<MB>(lam + v * MB, x);
-            const int e0 = g.col_ptr[v], e1 = g.col_ptr[v + 1];
-            for (int e = e0; e < e1; ++e) app += msg[(size_t)g.col_slot[e] * Q + x];
+            const uint32_t vp = sc.vn[v];
+            const int e0 = vp >> 8, e1 = e0 + (vp & 255);
+            for (int e = e0; e < e1; ++e) app += msg[(size_t)sc.vslot[e] * Q + x];
             const int d = group_argmin<Q>(app, x);
             if (x == 0) dec[v] = (uint8_t)d;
             for (int e = e0; e < e1; ++e) {
-                float *p = msg + (size_t)g.col_slot[e] * Q + x;
+                float *p = msg + (size_t)sc.vslot[e] * Q + x;
                 const float t = app - *p;
                 *p = t - group_min<Q>(t);
             }
         }
         __syncthreads();
-        fail = syndrome_fail<Q, MB>(g, dec, gmul);
+        fail = syndrome_fail<Q>(g, sc, dec, gmul);
         ++it;
     }
 
@@ -285,10 +303,13 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// dynamic LDS: [msg E*Q f32 (ems_lds only)] [lam N*m f32] [dec N u8] [gf_mul Q*Q u8] [gf_inv Q u8]
-static size_t aux_bytes(const NbDevGraph &g)
+// dynamic LDS: [msg E*Q f32 (ems_lds only)] [lam N*m f32] [dec N u8] [gf_mul Q*Q u8]
+//              [cn M u32] [vn N u32] [ecol E u16] [vslot E u16] [ehinv E u8] [eh E u8]
+__host__ __device__ inline size_t aux_bytes(const NbDevGraph &g)
 {
-    return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.q * g.q) + align16((size_t)g.q);
+    return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.q * g.q) +
+           align16((size_t)g.M * 4) + align16((size_t)g.N * 4) + 2 * align16((size_t)g.E * 2) +
+           2 * align16((size_t)g.E);
 }
 
 template <int Q, int MB, int DC, int SRC, bool GSTATE>
@@ -310,12 +331,32 @@ __global__ __launch_bounds__(1024) void k_ems(NbArgs a, NbDevGraph g, float *gsc
     p += align16((size_t)g.N);
     uint8_t *gmul = p;
     p += align16((size_t)Q * Q);
-    uint8_t *ginv = p;
+    uint32_t *cn = reinterpret_cast<uint32_t *>(p);
+    p += align16((size_t)g.M * 4);
+    uint32_t *vn = reinterpret_cast<uint32_t *>(p);
+    p += align16((size_t)g.N * 4);
+    uint16_t *ecol = reinterpret_cast<uint16_t *>(p);
+    p += align16((size_t)g.E * 2);
+    uint16_t *vslot = reinterpret_cast<uint16_t *>(p);
+    p += align16((size_t)g.E * 2);
+    uint8_t *ehinv = p;
+    p += align16((size_t)g.E);
+    uint8_t *eh = p;
     for (int i = threadIdx.x; i < Q * Q; i += blockDim.x) gmul[i] = g.gf_mul[i];
-    for (int i = threadIdx.x; i < Q; i += blockDim.x) ginv[i] = g.gf_inv[i];
+    for (int j = threadIdx.x; j < g.M; j += blockDim.x)
+        cn[j] = (uint32_t)g.row_ptr[j] | ((uint32_t)(g.row_ptr[j + 1] - g.row_ptr[j]) << 24);
+    for (int v = threadIdx.x; v < g.N; v += blockDim.x)
+        vn[v] = ((uint32_t)g.col_ptr[v] << 8) | (uint32_t)(g.col_ptr[v + 1] - g.col_ptr[v]);
+    for (int e = threadIdx.x; e < g.E; e += blockDim.x) {
+        ecol[e] = (uint16_t)g.row_col[e];
+        vslot[e] = (uint16_t)g.col_slot[e];
+        eh[e] = g.row_h[e];
+        ehinv[e] = g.gf_inv[g.row_h[e]];
+    }
     __syncthreads();
+    const NbSched sc{cn, ehinv, eh, ecol, vn, vslot};
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
-        ems_codeword<Q, MB, DC, SRC>(a, g, b, msg, lam, dec, gmul, ginv, red);
+        ems_codeword<Q, MB, DC, SRC>(a, g, b, msg, lam, dec, gmul, sc, red);
 }
 
 constexpr size_t kNbMaxLds = 160 * 1024;
@@ -326,6 +367,10 @@ NbChoice nb_choose(const NbDevGraph &g, int maxdc)
     ch.threads = 1024;
     ch.dc = maxdc <= 4 ? 4 : (maxdc <= 8 ? 8 : 16);
     const size_t aux = aux_bytes(g), msgb = align16((size_t)g.E * g.q * 4);
+    if (aux > kNbMaxLds || g.E > 65535 || g.N > 65535) {
+        ch.name = "";   // unsupported: the schedule does not fit LDS / 16-bit indices
+        return ch;
+    }
     if (aux + msgb <= kNbMaxLds) {
         ch.name = "ems_lds";
         ch.lds_bytes = (int)(aux + msgb);

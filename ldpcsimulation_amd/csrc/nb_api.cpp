@@ -267,6 +267,7 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
     if (max_batch <= 0) return err(LDPC_ERR_INVALID, "max_batch must be > 0");
     if (g->q != ldpc::kNbQ) return err(LDPC_ERR_UNSUPPORTED, "the EMS kernels are built for GF(16), got q=%d", g->q);
     if (g->maxdc > ldpc::kNbMaxDc) return err(LDPC_ERR_UNSUPPORTED, "row degree %d > %d", g->maxdc, ldpc::kNbMaxDc);
+    if (g->maxdv > 255) return err(LDPC_ERR_UNSUPPORTED, "column degree %d > 255", g->maxdv);
     int ndev = 0;
     NB_HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return err(LDPC_ERR_INVALID, "device %d outside 0..%d", device, ndev - 1);
@@ -321,6 +322,10 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
     c->dg.row_h = base + o_h;
     c->dg.gf_mul = base + o_mul;
     c->dg.gf_inv = base + o_inv;
+    if (!ldpc::nb_choose(c->dg, g->maxdc).name[0]) {
+        ldpc_nb_ctx_destroy(c);
+        return err(LDPC_ERR_UNSUPPORTED, "code too large for the EMS kernels (N=%d, E=%d)", g->N, g->E);
+    }
     NB_HIP_TRY(c->counts.ensure(8 * sizeof(unsigned long long)));
     NB_HIP_TRY(hipMemset(c->counts.p, 0, 8 * sizeof(unsigned long long)));
     *out = c;
