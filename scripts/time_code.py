@@ -30,7 +30,7 @@ def main():
     g = native.Graph.from_alist(a.alist)
     ctx = native.Context(g, 0, a.batch)
     v = {"ms": dict(variant=native.MS), "nms": dict(variant=native.NMS, alpha=1.25),
-         "oms": dict(variant=native.OMS, delta=0.15)}[a.variant]
+         "oms": dict(variant=native.OMS, delta=0.15), "bp": dict(variant=native.BP)}[a.variant]
     cfg = native.DecoderConfig(T=a.T, precision=native.F32 if a.prec == "f32" else native.F64,
                                schedule=native.LAYERED if a.schedule == "layered" else native.FLOODING, **v)
     if a.decoder == "gdbf":
