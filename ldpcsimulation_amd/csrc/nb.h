@@ -8,15 +8,17 @@
 namespace ldpc {
 
 constexpr int kNbQ = 16;          // field size the kernels are built for (GF(16), BASELINE config 5)
-constexpr int kNbMaxDc = 16;      // row degree bound (DC template 4 / 8 / 16)
+constexpr int kNbMaxDc = 8;       // row degree bound (DC template 4 / 8)
 
 struct NbDevGraph {
-    int N, M, q, m, E;
+    int N, M, q, m, E, maxdc;
     const int32_t *row_ptr;       // [M + 1]  edge slot of (check j, mlist position k) = row_ptr[j] + k
     const int32_t *row_col;       // [E]      symbol of each slot
     const uint8_t *row_h;         // [E]      GF(q) coefficient of each slot
     const int32_t *col_ptr;       // [N + 1]
-    const int32_t *col_slot;      // [E]      slots of each symbol, nlist order
+    const int32_t *col_slot;      // [E]      row-major slots of each symbol, nlist order
+    const int32_t *col_pslot;     // [E]      the same edges as position-major slots k*M + j
+    const uint8_t *col_h;         // [E]      their coefficients
     const uint8_t *gf_mul;        // [q * q]  multiplication table
     const uint8_t *gf_inv;        // [q]
 };

@@ -4,23 +4,25 @@
 // that does not compile). The algorithm is defined by the CPU oracle
 // oracle/ems_oracle.c, which this reproduces bit for bit.
 //
-// Mapping: a message is a 16-vector over GF(16); a group of 16 consecutive
-// lanes holds one message, lane x the entry of symbol x. Everything a check
-// or symbol node needs across the vector is a cross-lane move inside the
-// group, done with ds_swizzle in bitmask mode (no LDS traffic):
-//   broadcast of lane a   ->  and = 0x10, or = a
-//   lane x reads lane x^a ->  and = 0x1F, xor = a
-// so the elementary check node W(x) = min_a P(a) + Q(a ^ x) is 16 steps of
-// (swizzle, swizzle, add, min) per lane. One workgroup = 1024 threads =
-// 64 groups decodes one codeword at a time (persistent over the batch); the
-// codeword's edge messages (E x 16 fp32, in place: c2v after the check phase,
-// v2c after the symbol phase) and bit LLRs live in LDS when they fit
-// (145 KB for N = 1000, E = 2000), else in a global slot per workgroup.
+// Mapping. Check nodes: one lane per (check, direction) holds whole 16-entry
+// message vectors in registers, so the elementary check node
+// W(x) = min_a P(a) + R(a ^ x) is 256 register adds and mins with no
+// cross-lane traffic; the two lanes of a check split the forward-backward
+// (see cn_lane). Symbol nodes: a group of 16 consecutive lanes per symbol,
+// lane x = symbol x, with argmin/min butterflies done by ds_swizzle in
+// bitmask mode (lane x reads lane x^a: and = 0x1F, xor = a). One workgroup
+// decodes one codeword at a time (persistent over the batch); its edge
+// messages (16 fp32 per edge, in place: c2v after the check phase, v2c after
+// the symbol phase, kept in the check domain) and bit LLRs live in LDS when
+// they fit (128 KB of messages for N = 1000, E = 2000), else in a global
+// slot per workgroup.
 #include "nb.h"
 #include "device_common.h"
 #include "kernels.h"
 
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 namespace ldpc {
 
@@ -39,49 +41,6 @@ __device__ __forceinline__ int swz(int v)
 // lane x of a Q-lane group reads lane x ^ X / lane A of its group
 template <int Q, int X> struct XorPat { static constexpr int v = (X << 10) | 0x1F; };
 template <int Q, int A> struct BcastPat { static constexpr int v = (A << 5) | (0x1F & ~(Q - 1)); };
-
-// W(x) = min over a of P(a) + Q(a ^ x)  (oracle ecn(): the same single adds, exact min)
-template <int Q, int A>
-struct Ecn {
-    static __device__ __forceinline__ float run(float p, float qv, float w)
-    {
-        const float s = swz<BcastPat<Q, A>::v>(p) + swz<XorPat<Q, A>::v>(qv);
-        return Ecn<Q, A + 1>::run(p, qv, fminf(w, s));
-    }
-};
-template <int Q>
-struct Ecn<Q, Q> {
-    static __device__ __forceinline__ float run(float, float, float w) { return w; }
-};
-
-// number of lanes y != x with (v_y, y) < (v_x, x)
-template <int Q, int X>
-struct Rank {
-    static __device__ __forceinline__ int run(float v, int x, int r)
-    {
-        const float o = swz<XorPat<Q, X>::v>(v);
-        const int y = x ^ X;
-        r += (o < v) | ((o == v) & (y < x));
-        return Rank<Q, X + 1>::run(v, x, r);
-    }
-};
-template <int Q>
-struct Rank<Q, Q> {
-    static __device__ __forceinline__ int run(float, int, int r) { return r; }
-};
-
-template <int Q>
-__device__ __forceinline__ float trunc_nm(float v, int x, int nm)
-{
-    if (nm >= Q) return v;
-    return Rank<Q, 1>::run(v, x, 0) < nm ? v : kInf;
-}
-
-template <int Q>
-__device__ __forceinline__ float ecn(float p, float qv)
-{
-    return Ecn<Q, 0>::run(p, qv, kInf);
-}
 
 template <int Q>
 __device__ __forceinline__ float group_min(float v)
@@ -139,16 +98,24 @@ __device__ __forceinline__ float sym_llr(const float *lam, int x)
 }
 
 // The graph, re-packed into LDS once per workgroup (global loads in the
-// per-iteration loops would put two dependent HBM/L2 round trips on every
-// check and symbol round).
+// per-iteration loops would put dependent L2 round trips on every round).
+// Edge slots are position-major: slot(j, k) = k*M + j for check j and mlist
+// position k, so the check-node lanes of a wave (consecutive j, same k) read
+// consecutive 16-byte chunks. Messages are stored in the CHECK domain,
+// chunk-major: entry x of slot s at float ((x >> 2) * Ep + s) * 4 + (x & 3),
+// with Ep = slots rounded to 2 mod 8 (spreads the symbol-node gathers over
+// the banks).
 struct NbSched {
-    const uint32_t *cn;      // [M]  r0 | d << 24
-    const uint8_t *ehinv;    // [E]  h^-1 of each edge slot
-    const uint8_t *eh;       // [E]  h
-    const uint16_t *ecol;    // [E]  symbol of each edge slot
-    const uint32_t *vn;      // [N]  first col entry << 8 | degree
-    const uint16_t *vslot;   // [E]  edge slots of each symbol, nlist order
+    int Ep;
+    const uint8_t *cn_d;     // [M]    check degree
+    const uint16_t *ecol;    // [Ms]   symbol of each slot (syndrome)
+    const uint8_t *eh;       // [Ms]   coefficient of each slot
+    const uint32_t *vn;      // [N]    first col entry << 8 | degree
+    const uint16_t *vslot;   // [E]    slots of each symbol, nlist order
+    const uint8_t *vh;       // [E]    their coefficients
 };
+
+__device__ __forceinline__ int msg_index(int Ep, int slot, int x) { return (((x >> 2) * Ep + slot) << 2) + (x & 3); }
 
 template <int Q>
 __device__ __forceinline__ int syndrome_fail(const NbDevGraph &g, const NbSched &s, const uint8_t *dec,
@@ -156,13 +123,126 @@ __device__ __forceinline__ int syndrome_fail(const NbDevGraph &g, const NbSched 
 {
     int fail = 0;
     for (int j = threadIdx.x; j < g.M; j += blockDim.x) {
-        const uint32_t sc = s.cn[j];
-        const int r0 = sc & 0xFFFFFF, d = sc >> 24;
+        const int d = s.cn_d[j];
         int sy = 0;
-        for (int e = r0; e < r0 + d; ++e) sy ^= gmul[s.eh[e] * Q + dec[s.ecol[e]]];
+        for (int k = 0; k < d; ++k) {
+            const int sl = k * g.M + j;
+            sy ^= gmul[s.eh[sl] * Q + dec[s.ecol[sl]]];
+        }
         fail |= sy != 0;
     }
     return __syncthreads_or(fail);
+}
+
+// ---- check node: one lane per (check, direction), the message vectors in registers ----
+template <int Q>
+__device__ __forceinline__ void load_vec(const float *msg, int Ep, int slot, float (&v)[Q])
+{
+#pragma unroll
+    for (int c = 0; c < Q / 4; ++c) {
+        const float4 t = *reinterpret_cast<const float4 *>(msg + ((c * Ep + slot) << 2));
+        v[4 * c] = t.x;
+        v[4 * c + 1] = t.y;
+        v[4 * c + 2] = t.z;
+        v[4 * c + 3] = t.w;
+    }
+}
+
+// keep the nm smallest entries by (value, symbol), the rest -> +inf (oracle trunc_nm)
+template <int Q>
+__device__ __forceinline__ void trunc_vec(float (&v)[Q], int nm)
+{
+    if (nm >= Q) return;
+    int r[Q];
+#pragma unroll
+    for (int x = 0; x < Q; ++x) {
+        int c = 0;
+#pragma unroll
+        for (int y = 0; y < Q; ++y)
+            if (y < x)
+                c += v[y] <= v[x];
+            else if (y > x)
+                c += v[y] < v[x];
+        r[x] = c;
+    }
+#pragma unroll
+    for (int x = 0; x < Q; ++x) v[x] = r[x] < nm ? v[x] : kInf;
+}
+
+// W(x) = min_a P(a) + R(a ^ x): the oracle's ecn(), the same single adds, exact min
+template <int Q>
+__device__ __forceinline__ void ecn_reg(const float (&P)[Q], const float (&R)[Q], float (&W)[Q])
+{
+#pragma unroll
+    for (int x = 0; x < Q; ++x) {
+        float w = P[0] + R[x];
+#pragma unroll
+        for (int a = 1; a < Q; ++a) w = fminf(w, P[a] + R[a ^ x]);
+        W[x] = w;
+    }
+}
+
+// fill absent (+inf) entries with max finite + offset, then store
+template <int Q>
+__device__ __forceinline__ void store_out(float *msg, int Ep, int slot, float (&w)[Q], int nm, float offset)
+{
+    if (nm < Q) {
+        float mx = -1.0f;
+#pragma unroll
+        for (int x = 0; x < Q; ++x) mx = fmaxf(mx, w[x] < kInf ? w[x] : -1.0f);
+#pragma unroll
+        for (int x = 0; x < Q; ++x) w[x] = w[x] < kInf ? w[x] : mx + offset;
+    }
+#pragma unroll
+    for (int c = 0; c < Q / 4; ++c)
+        *reinterpret_cast<float4 *>(msg + ((c * Ep + slot) << 2)) =
+            make_float4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+}
+
+// Forward-backward EMS of one check of degree D, split over two lanes of the
+// same wave: dir = 0 walks the edges in mlist order, dir = 1 in reverse (its
+// forward chain is the oracle's backward chain B; ECN is symmetric in its
+// operands, each sum being one commutative add). Each lane writes the
+// outputs of its half: own positions lo .. D-1, lo = ceil(D/2) / floor(D/2).
+// In place and race-free: the two lanes run the same instruction stream in
+// lockstep, and a re-read of an input (own position kp, kp > (D-1)/2) never
+// meets a position the partner lane has already written (positions >= kp of
+// its own order, i.e. <= D-1-kp < kp of ours).
+template <int Q, int D>
+__device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int dir, int nm, float offset)
+{
+    auto slot = [&](int kp) { return (dir ? D - 1 - kp : kp) * M + j; };
+    float F[D - 1][Q];
+    float U[Q], B[Q], W[Q];
+    load_vec<Q>(msg, Ep, slot(0), F[0]);
+    trunc_vec<Q>(F[0], nm);
+#pragma unroll
+    for (int kp = 1; kp <= D - 2; ++kp) {
+        load_vec<Q>(msg, Ep, slot(kp), U);
+        trunc_vec<Q>(U, nm);
+        ecn_reg<Q>(F[kp - 1], U, F[kp]);
+        trunc_vec<Q>(F[kp], nm);
+    }
+    const int lo = dir ? D / 2 : (D + 1) / 2;
+    load_vec<Q>(msg, Ep, slot(D - 1), B);
+    trunc_vec<Q>(B, nm);
+#pragma unroll
+    for (int kp = D - 2; kp >= 1; --kp) {
+        if (kp >= lo) {
+            ecn_reg<Q>(F[kp - 1], B, W);
+            trunc_vec<Q>(W, nm);
+            store_out<Q>(msg, Ep, slot(kp), W, nm, offset);
+            if (kp - 1 >= lo) {
+                load_vec<Q>(msg, Ep, slot(kp), U);
+                trunc_vec<Q>(U, nm);
+                ecn_reg<Q>(B, U, W);
+                trunc_vec<Q>(W, nm);
+#pragma unroll
+                for (int x = 0; x < Q; ++x) B[x] = W[x];
+            }
+        }
+    }
+    store_out<Q>(msg, Ep, slot(D - 1), F[D - 2], nm, offset);
 }
 
 template <int Q, int MB, int DC, int SRC>
@@ -171,7 +251,7 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
 {
     const int tid = threadIdx.x, nt = blockDim.x;
     const int x = tid & (Q - 1), grp = tid / Q, ngrp = nt / Q;
-    const int N = g.N, M = g.M;
+    const int N = g.N, M = g.M, Ep = sc.Ep;
     const uint64_t cw = a.first_cw + (uint64_t)b;
     const uint8_t *cvec = (SRC == SRC_GIVEN && a.c) ? a.c + (size_t)b * N : nullptr;
 
@@ -208,67 +288,53 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         }
     }
     __syncthreads();
-    // ---- initial messages v2c = L, decisions argmin L ----
+    // ---- initial messages v2c = L (stored at the check-domain position h*x), decisions argmin L ----
     for (int v = grp; v < N; v += ngrp) {
         const float L = sym_llr<MB>(lam + v * MB, x);
         const uint32_t vp = sc.vn[v];
         const int e0 = vp >> 8, e1 = e0 + (vp & 255);
-        for (int e = e0; e < e1; ++e) msg[(size_t)sc.vslot[e] * Q + x] = L;
+        for (int e = e0; e < e1; ++e) msg[msg_index(Ep, sc.vslot[e], gmul[sc.vh[e] * Q + x])] = L;
         const int d = group_argmin<Q>(L, x);
         if (x == 0) dec[v] = (uint8_t)d;
     }
     __syncthreads();
     int fail = syndrome_fail<Q>(g, sc, dec, gmul);
     int it = 0;
+    // check lanes: in each wave, lanes 0-31 take 32 consecutive checks in mlist
+    // order and lanes 32-63 the same checks reversed
+    const int cdir = (tid >> 5) & 1, cpr = (nt >> 6) * 32;
+    const int cj0 = (tid >> 6) * 32 + (tid & 31);
     while (it < a.T && (!a.early_stop || fail)) {
-        // ---- check nodes: forward-backward EMS ----
-        for (int j = grp; j < M; j += ngrp) {
-            const uint32_t cs = sc.cn[j];
-            const int r0 = cs & 0xFFFFFF, d = cs >> 24;
-            float U[DC], F[DC], B[DC];
-            int idx[DC];
-#pragma unroll
-            for (int k = 0; k < DC; ++k)
-                if (k < d) {
-                    idx[k] = (r0 + k) * Q + gmul[sc.ehinv[r0 + k] * Q + x];   // U(x) = v2c(h^-1 x)
-                    U[k] = trunc_nm<Q>(msg[idx[k]], x, a.nm);
+        // ---- check nodes ----
+        for (int j = cj0; j < M; j += cpr) {
+            switch (sc.cn_d[j]) {
+            case 2: cn_lane<Q, 2>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
+            case 3: cn_lane<Q, 3>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
+            case 4: cn_lane<Q, 4>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
+            default:
+                if (DC > 4) {
+                    switch (sc.cn_d[j]) {
+                    case 5: cn_lane<Q, DC >= 5 ? 5 : 2>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
+                    case 6: cn_lane<Q, DC >= 6 ? 6 : 2>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
+                    case 7: cn_lane<Q, DC >= 7 ? 7 : 2>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
+                    case 8: cn_lane<Q, DC >= 8 ? 8 : 2>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
+                    default: break;
+                    }
                 }
-            F[0] = U[0];
-#pragma unroll
-            for (int k = 1; k < DC - 1; ++k)
-                if (k <= d - 2) F[k] = trunc_nm<Q>(ecn<Q>(F[k - 1], U[k]), x, a.nm);
-#pragma unroll
-            for (int k = DC - 1; k >= 1; --k) {
-                if (k == d - 1)
-                    B[k] = U[k];
-                else if (k < d - 1)
-                    B[k] = trunc_nm<Q>(ecn<Q>(B[k + 1 < DC ? k + 1 : k], U[k]), x, a.nm);
+                break;
             }
-#pragma unroll
-            for (int k = 0; k < DC; ++k)
-                if (k < d) {
-                    float w;
-                    if (k == 0)
-                        w = B[1];
-                    else if (k == d - 1)
-                        w = F[k - 1];
-                    else
-                        w = trunc_nm<Q>(ecn<Q>(F[k - 1], B[k + 1 < DC ? k + 1 : k]), x, a.nm);
-                    const float mx = group_max<Q>(w < kInf ? w : -1.0f);
-                    msg[idx[k]] = w < kInf ? w : mx + a.offset;        // c2v(a) = W(h a), a = h^-1 x
-                }
         }
         __syncthreads();
-        // ---- symbol nodes ----
+        // ---- symbol nodes: lane x = variable-domain symbol, reads c2v(x) at position h*x ----
         for (int v = grp; v < N; v += ngrp) {
             float app = sym_llr<MB>(lam + v * MB, x);
             const uint32_t vp = sc.vn[v];
             const int e0 = vp >> 8, e1 = e0 + (vp & 255);
-            for (int e = e0; e < e1; ++e) app += msg[(size_t)sc.vslot[e] * Q + x];
+            for (int e = e0; e < e1; ++e) app += msg[msg_index(Ep, sc.vslot[e], gmul[sc.vh[e] * Q + x])];
             const int d = group_argmin<Q>(app, x);
             if (x == 0) dec[v] = (uint8_t)d;
             for (int e = e0; e < e1; ++e) {
-                float *p = msg + (size_t)sc.vslot[e] * Q + x;
+                float *p = msg + msg_index(Ep, sc.vslot[e], gmul[sc.vh[e] * Q + x]);
                 const float t = app - *p;
                 *p = t - group_min<Q>(t);
             }
@@ -303,27 +369,33 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// dynamic LDS: [msg E*Q f32 (ems_lds only)] [lam N*m f32] [dec N u8] [gf_mul Q*Q u8]
-//              [cn M u32] [vn N u32] [ecol E u16] [vslot E u16] [ehinv E u8] [eh E u8]
+// Position-major slot count (maxdc * M) padded to 2 mod 8.
+__host__ __device__ inline int nb_ep(const NbDevGraph &g) { return (g.maxdc * g.M + 5) / 8 * 8 + 2; }
+
+// dynamic LDS: [msg 16*Ep f32 (ems_lds only)] [lam N*m f32] [dec N u8] [gf_mul Q*Q u8] [cn_d M u8]
+//              [ecol Ms u16] [eh Ms u8] [vn N u32] [vslot E u16] [vh E u8]
 __host__ __device__ inline size_t aux_bytes(const NbDevGraph &g)
 {
-    return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.q * g.q) +
-           align16((size_t)g.M * 4) + align16((size_t)g.N * 4) + 2 * align16((size_t)g.E * 2) +
-           2 * align16((size_t)g.E);
+    const size_t ms = (size_t)g.maxdc * g.M;
+    return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.q * g.q) + align16((size_t)g.M) +
+           align16(ms * 2) + align16(ms) + align16((size_t)g.N * 4) + align16((size_t)g.E * 2) + align16((size_t)g.E);
 }
 
-template <int Q, int MB, int DC, int SRC, bool GSTATE>
-__global__ __launch_bounds__(1024) void k_ems(NbArgs a, NbDevGraph g, float *gscratch, size_t slot_floats)
+template <int Q, int MB, int DC, int SRC, bool GSTATE, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *gscratch,
+                                                            size_t slot_floats)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int red[16 * 3];
+    const int Ep = nb_ep(g);
+    const size_t ms = (size_t)g.maxdc * g.M;
     unsigned char *p = smem;
     float *msg;
     if (GSTATE) {
         msg = gscratch + slot_floats * blockIdx.x;
     } else {
         msg = reinterpret_cast<float *>(p);
-        p += align16((size_t)g.E * Q * 4);
+        p += align16((size_t)Ep * Q * 4);
     }
     float *lam = reinterpret_cast<float *>(p);
     p += align16((size_t)g.N * MB * 4);
@@ -331,30 +403,34 @@ __global__ __launch_bounds__(1024) void k_ems(NbArgs a, NbDevGraph g, float *gsc
     p += align16((size_t)g.N);
     uint8_t *gmul = p;
     p += align16((size_t)Q * Q);
-    uint32_t *cn = reinterpret_cast<uint32_t *>(p);
-    p += align16((size_t)g.M * 4);
+    uint8_t *cn_d = p;
+    p += align16((size_t)g.M);
+    uint16_t *ecol = reinterpret_cast<uint16_t *>(p);
+    p += align16(ms * 2);
+    uint8_t *eh = p;
+    p += align16(ms);
     uint32_t *vn = reinterpret_cast<uint32_t *>(p);
     p += align16((size_t)g.N * 4);
-    uint16_t *ecol = reinterpret_cast<uint16_t *>(p);
-    p += align16((size_t)g.E * 2);
     uint16_t *vslot = reinterpret_cast<uint16_t *>(p);
     p += align16((size_t)g.E * 2);
-    uint8_t *ehinv = p;
-    p += align16((size_t)g.E);
-    uint8_t *eh = p;
+    uint8_t *vh = p;
     for (int i = threadIdx.x; i < Q * Q; i += blockDim.x) gmul[i] = g.gf_mul[i];
-    for (int j = threadIdx.x; j < g.M; j += blockDim.x)
-        cn[j] = (uint32_t)g.row_ptr[j] | ((uint32_t)(g.row_ptr[j + 1] - g.row_ptr[j]) << 24);
+    for (int j = threadIdx.x; j < g.M; j += blockDim.x) {
+        const int r0 = g.row_ptr[j], d = g.row_ptr[j + 1] - r0;
+        cn_d[j] = (uint8_t)d;
+        for (int k = 0; k < d; ++k) {
+            ecol[k * g.M + j] = (uint16_t)g.row_col[r0 + k];
+            eh[k * g.M + j] = g.row_h[r0 + k];
+        }
+    }
     for (int v = threadIdx.x; v < g.N; v += blockDim.x)
         vn[v] = ((uint32_t)g.col_ptr[v] << 8) | (uint32_t)(g.col_ptr[v + 1] - g.col_ptr[v]);
     for (int e = threadIdx.x; e < g.E; e += blockDim.x) {
-        ecol[e] = (uint16_t)g.row_col[e];
-        vslot[e] = (uint16_t)g.col_slot[e];
-        eh[e] = g.row_h[e];
-        ehinv[e] = g.gf_inv[g.row_h[e]];
+        vslot[e] = (uint16_t)g.col_pslot[e];
+        vh[e] = g.col_h[e];
     }
     __syncthreads();
-    const NbSched sc{cn, ehinv, eh, ecol, vn, vslot};
+    const NbSched sc{Ep, cn_d, ecol, eh, vn, vslot, vh};
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
         ems_codeword<Q, MB, DC, SRC>(a, g, b, msg, lam, dec, gmul, sc, red);
 }
@@ -364,11 +440,19 @@ constexpr size_t kNbMaxLds = 160 * 1024;
 NbChoice nb_choose(const NbDevGraph &g, int maxdc)
 {
     NbChoice ch;
-    ch.threads = 1024;
-    ch.dc = maxdc <= 4 ? 4 : (maxdc <= 8 ? 8 : 16);
-    const size_t aux = aux_bytes(g), msgb = align16((size_t)g.E * g.q * 4);
-    if (aux > kNbMaxLds || g.E > 65535 || g.N > 65535) {
-        ch.name = "";   // unsupported: the schedule does not fit LDS / 16-bit indices
+    ch.dc = maxdc <= 4 ? 4 : 8;
+    // 512 threads: the register-resident check node needs up to ~180 VGPRs
+    // (1024-thread blocks cap a wave at 128 and spill); LDS allows one
+    // workgroup per CU either way. LDPC_EMS_THREADS=1024 selects the other
+    // build for DC = 4 (A/B only).
+    ch.threads = 512;
+    if (ch.dc == 4) {
+        const char *e = std::getenv("LDPC_EMS_THREADS");
+        if (e && std::atoi(e) == 1024) ch.threads = 1024;
+    }
+    const size_t aux = aux_bytes(g), msgb = align16((size_t)nb_ep(g) * g.q * 4);
+    if (maxdc > kNbMaxDc || aux > kNbMaxLds || nb_ep(g) > 65535 || g.N > 65535) {
+        ch.name = "";   // unsupported: degree, LDS schedule or 16-bit indices
         return ch;
     }
     if (aux + msgb <= kNbMaxLds) {
@@ -386,7 +470,7 @@ template <int DC, int SRC, bool GS>
 static hipError_t launch_t(const NbDevGraph &g, const NbArgs &a, const NbChoice &ch, void *scratch, int grid,
                            hipStream_t s)
 {
-    auto fn = k_ems<kNbQ, 4, DC, SRC, GS>;
+    auto fn = (DC == 4 && ch.threads == 1024) ? k_ems<kNbQ, 4, DC, SRC, GS, 1024> : k_ems<kNbQ, 4, DC, SRC, GS, 512>;
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, ch.lds_bytes);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(ch.threads), ch.lds_bytes, s, a, g, (float *)scratch,
@@ -410,7 +494,7 @@ hipError_t nb_launch(const NbDevGraph &g, const NbArgs &a, const NbChoice &ch, v
                      int num_cus, hipStream_t s)
 {
     if (a.batch <= 0) return hipSuccess;
-    if (g.q != kNbQ || g.m != 4) return hipErrorInvalidValue;
+    if (g.q != kNbQ || g.m != 4 || !ch.name[0]) return hipErrorInvalidValue;
     int grid;
     if (ch.slot_bytes) {
         if (!scratch || slots <= 0) return hipErrorInvalidValue;
@@ -420,11 +504,7 @@ hipError_t nb_launch(const NbDevGraph &g, const NbArgs &a, const NbChoice &ch, v
         grid = per_cu * num_cus;
         if (grid > a.batch) grid = a.batch;
     }
-    switch (ch.dc) {
-    case 4: return launch_dc<4>(g, a, ch, scratch, grid, s);
-    case 8: return launch_dc<8>(g, a, ch, scratch, grid, s);
-    default: return launch_dc<16>(g, a, ch, scratch, grid, s);
-    }
+    return ch.dc == 4 ? launch_dc<4>(g, a, ch, scratch, grid, s) : launch_dc<8>(g, a, ch, scratch, grid, s);
 }
 
 }  // namespace ldpc

@@ -293,7 +293,17 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
             if (mul[(size_t)a * q + b] == 1) inv[a] = (uint8_t)b;
         }
     const size_t n_rp = (g->M + 1) * 4, n_rc = (size_t)g->E * 4, n_cp = (g->N + 1) * 4, n_cs = (size_t)g->E * 4;
-    const size_t total = n_rp + n_rc + n_cp + n_cs + g->E + mul.size() + inv.size() + 64;
+    // position-major slot (k*M + j) and coefficient of every column entry
+    std::vector<int32_t> pslot(g->E);
+    std::vector<uint8_t> colh(g->E);
+    for (int j = 0; j < g->M; ++j)
+        for (int r = g->row_ptr[j]; r < g->row_ptr[j + 1]; ++r)
+            for (int e = g->col_ptr[g->row_col[r]]; e < g->col_ptr[g->row_col[r] + 1]; ++e)
+                if (g->col_slot[e] == r) {
+                    pslot[e] = (r - g->row_ptr[j]) * g->M + j;
+                    colh[e] = g->row_h[r];
+                }
+    const size_t total = n_rp + n_rc + n_cp + 2 * n_cs + 2 * (size_t)g->E + mul.size() + inv.size() + 256;
     std::vector<uint8_t> blob(total, 0);
     size_t off = 0;
     auto put = [&](const void *src, size_t n) {
@@ -306,7 +316,8 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
     const size_t o_rp = put(g->row_ptr.data(), n_rp), o_rc = put(g->row_col.data(), n_rc),
                  o_cp = put(g->col_ptr.data(), n_cp), o_cs = put(g->col_slot.data(), n_cs),
                  o_h = put(g->row_h.data(), g->E), o_mul = put(mul.data(), mul.size()),
-                 o_inv = put(inv.data(), inv.size());
+                 o_inv = put(inv.data(), inv.size()), o_ps = put(pslot.data(), n_cs),
+                 o_ch = put(colh.data(), g->E);
     NB_HIP_TRY(c->graph.ensure(off));
     NB_HIP_TRY(hipMemcpy(c->graph.p, blob.data(), off, hipMemcpyHostToDevice));
     auto *base = (uint8_t *)c->graph.p;
@@ -322,6 +333,9 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
     c->dg.row_h = base + o_h;
     c->dg.gf_mul = base + o_mul;
     c->dg.gf_inv = base + o_inv;
+    c->dg.col_pslot = (const int32_t *)(base + o_ps);
+    c->dg.col_h = base + o_ch;
+    c->dg.maxdc = g->maxdc;
     if (!ldpc::nb_choose(c->dg, g->maxdc).name[0]) {
         ldpc_nb_ctx_destroy(c);
         return err(LDPC_ERR_UNSUPPORTED, "code too large for the EMS kernels (N=%d, E=%d)", g->N, g->E);
