@@ -4,18 +4,19 @@
 // that does not compile). The algorithm is defined by the CPU oracle
 // oracle/ems_oracle.c, which this reproduces bit for bit.
 //
-// Mapping. Check nodes: one lane per (check, direction) holds whole 16-entry
-// message vectors in registers, so the elementary check node
-// W(x) = min_a P(a) + R(a ^ x) is 256 register adds and mins with no
-// cross-lane traffic; the two lanes of a check split the forward-backward
-// (see cn_lane). Symbol nodes: a group of 16 consecutive lanes per symbol,
-// lane x = symbol x, with argmin/min butterflies done by ds_swizzle in
-// bitmask mode (lane x reads lane x^a: and = 0x1F, xor = a). One workgroup
-// decodes one codeword at a time (persistent over the batch); its edge
-// messages (16 fp32 per edge, in place: c2v after the check phase, v2c after
-// the symbol phase, kept in the check domain) and bit LLRs live in LDS when
-// they fit (128 KB of messages for N = 1000, E = 2000), else in a global
-// slot per workgroup.
+// Mapping: every node works on whole 16-entry message vectors held in the
+// registers of ONE lane, so no cross-lane traffic is needed.
+//   check node: one lane per (check, direction); the elementary check node
+//     W(x) = min_a P(a) + R(a ^ x) is 256 register adds and mins, and the two
+//     lanes of a check (same wave, lockstep) split the forward-backward
+//     (cn_lane); messages are read and written as 4 x 16-byte chunks;
+//   symbol node: one lane per symbol, entry a of an edge gathered from its
+//     check-domain position h*a (GF(16) products by xtime in registers).
+// One 512-thread workgroup decodes one codeword at a time (persistent over
+// the batch); its edge messages (16 fp32 per edge, in place: c2v after the
+// check phase, v2c after the symbol phase) and bit LLRs live in LDS when they
+// fit (128 KB of messages for N = 1000, E = 2000), else in a global slot per
+// workgroup.
 #include "nb.h"
 #include "device_common.h"
 #include "kernels.h"
@@ -27,75 +28,6 @@
 namespace ldpc {
 
 constexpr float kInf = __builtin_huge_valf();
-
-template <int PAT>
-__device__ __forceinline__ float swz(float v)
-{
-    return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), PAT));
-}
-template <int PAT>
-__device__ __forceinline__ int swz(int v)
-{
-    return __builtin_amdgcn_ds_swizzle(v, PAT);
-}
-// lane x of a Q-lane group reads lane x ^ X / lane A of its group
-template <int Q, int X> struct XorPat { static constexpr int v = (X << 10) | 0x1F; };
-template <int Q, int A> struct BcastPat { static constexpr int v = (A << 5) | (0x1F & ~(Q - 1)); };
-
-template <int Q>
-__device__ __forceinline__ float group_min(float v)
-{
-    v = fminf(v, swz<XorPat<Q, 1>::v>(v));
-    v = fminf(v, swz<XorPat<Q, 2>::v>(v));
-    v = fminf(v, swz<XorPat<Q, 4>::v>(v));
-    if (Q > 8) v = fminf(v, swz<XorPat<Q, 8>::v>(v));
-    return v;
-}
-template <int Q>
-__device__ __forceinline__ float group_max(float v)
-{
-    v = fmaxf(v, swz<XorPat<Q, 1>::v>(v));
-    v = fmaxf(v, swz<XorPat<Q, 2>::v>(v));
-    v = fmaxf(v, swz<XorPat<Q, 4>::v>(v));
-    if (Q > 8) v = fmaxf(v, swz<XorPat<Q, 8>::v>(v));
-    return v;
-}
-// first minimum: smallest (value, symbol)
-template <int Q, int X>
-__device__ __forceinline__ void argmin_step(float &bv, int &bi)
-{
-    const float ov = swz<XorPat<Q, X>::v>(bv);
-    const int oi = swz<XorPat<Q, X>::v>(bi);
-    if (ov < bv || (ov == bv && oi < bi)) {
-        bv = ov;
-        bi = oi;
-    }
-}
-template <int Q>
-__device__ __forceinline__ int group_argmin(float v, int x)
-{
-    float bv = v;
-    int bi = x;
-    argmin_step<Q, 1>(bv, bi);
-    argmin_step<Q, 2>(bv, bi);
-    argmin_step<Q, 4>(bv, bi);
-    if (Q > 8) argmin_step<Q, 8>(bv, bi);
-    return bi;
-}
-
-// L(x) = sum over bits i (ascending) disagreeing with the hard decision of |lam_i| (oracle symbol_llr)
-template <int MB>
-__device__ __forceinline__ float sym_llr(const float *lam, int x)
-{
-    float s = 0.0f;
-#pragma unroll
-    for (int i = 0; i < MB; ++i) {
-        const float l = lam[i];
-        const int hd = l < 0.0f;
-        if (((x >> i) & 1) != hd) s += fabsf(l);
-    }
-    return s;
-}
 
 // The graph, re-packed into LDS once per workgroup (global loads in the
 // per-iteration loops would put dependent L2 round trips on every round).
@@ -114,8 +46,6 @@ struct NbSched {
     const uint16_t *vslot;   // [E]    slots of each symbol, nlist order
     const uint8_t *vh;       // [E]    their coefficients
 };
-
-__device__ __forceinline__ int msg_index(int Ep, int slot, int x) { return (((x >> 2) * Ep + slot) << 2) + (x & 3); }
 
 template <int Q>
 __device__ __forceinline__ int syndrome_fail(const NbDevGraph &g, const NbSched &s, const uint8_t *dec,
@@ -245,12 +175,83 @@ __device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int di
     store_out<Q>(msg, Ep, slot(D - 1), F[D - 2], nm, offset);
 }
 
+// GF(16) products h*a for a = 0..15 (x^4 + x + 1): h*2^i by xtime, then the
+// xor of the powers in a.
+__device__ __forceinline__ int gf16_xt(int v) { return ((v << 1) & 15) ^ ((v & 8) ? 3 : 0); }
+
+// ---- symbol node: one lane per symbol, the 16-entry vectors in registers ----
+// Entry a (symbol domain) of an edge's message lives at check-domain position
+// h*a. init: write v2c = L on every edge. Otherwise app = L + sum of the c2v
+// (nlist order), decision argmin app (first minimum), v2c = (app - c2v) - min.
+template <int Q, int MB>
+__device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched &sc, const float *lam, uint8_t *dec,
+                                        bool init)
+{
+    static_assert(Q == 16 && MB == 4, "GF(16)");
+    const float4 l4 = *reinterpret_cast<const float4 *>(lam + v * MB);
+    const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+    float app[Q];
+#pragma unroll
+    for (int a = 0; a < Q; ++a) {
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < MB; ++i)
+            if (((a >> i) & 1) != (lv[i] < 0.0f)) s += fabsf(lv[i]);   // oracle symbol_llr
+        app[a] = s;
+    }
+    const uint32_t vp = sc.vn[v];
+    const int e0 = vp >> 8, e1 = e0 + (vp & 255);
+    auto addr = [&](int e, int (&ad)[Q]) {
+        const int s = sc.vslot[e], h1 = sc.vh[e];
+        const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
+#pragma unroll
+        for (int a = 0; a < Q; ++a) {
+            const int p = ((a & 1) ? h1 : 0) ^ ((a & 2) ? h2 : 0) ^ ((a & 4) ? h4 : 0) ^ ((a & 8) ? h8 : 0);
+            ad[a] = (((p >> 2) * Ep + s) << 2) + (p & 3);
+        }
+    };
+    int ad[Q];
+    if (init) {
+        for (int e = e0; e < e1; ++e) {
+            addr(e, ad);
+#pragma unroll
+            for (int a = 0; a < Q; ++a) msg[ad[a]] = app[a];
+        }
+    } else {
+        for (int e = e0; e < e1; ++e) {
+            addr(e, ad);
+#pragma unroll
+            for (int a = 0; a < Q; ++a) app[a] += msg[ad[a]];
+        }
+    }
+    int best = 0;
+    float bv = app[0];
+#pragma unroll
+    for (int a = 1; a < Q; ++a)
+        if (app[a] < bv) {
+            bv = app[a];
+            best = a;
+        }
+    dec[v] = (uint8_t)best;
+    if (init) return;
+    for (int e = e0; e < e1; ++e) {
+        addr(e, ad);
+        float t[Q], mn = kInf;
+#pragma unroll
+        for (int a = 0; a < Q; ++a) {
+            t[a] = app[a] - msg[ad[a]];
+            mn = fminf(mn, t[a]);
+        }
+#pragma unroll
+        for (int a = 0; a < Q; ++a) msg[ad[a]] = t[a] - mn;
+    }
+}
+
 template <int Q, int MB, int DC, int SRC>
 __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &g, int b, float *msg, float *lam,
                                              uint8_t *dec, const uint8_t *gmul, const NbSched &sc, int *red)
 {
     const int tid = threadIdx.x, nt = blockDim.x;
-    const int x = tid & (Q - 1), grp = tid / Q, ngrp = nt / Q;
     const int N = g.N, M = g.M, Ep = sc.Ep;
     const uint64_t cw = a.first_cw + (uint64_t)b;
     const uint8_t *cvec = (SRC == SRC_GIVEN && a.c) ? a.c + (size_t)b * N : nullptr;
@@ -289,14 +290,7 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     }
     __syncthreads();
     // ---- initial messages v2c = L (stored at the check-domain position h*x), decisions argmin L ----
-    for (int v = grp; v < N; v += ngrp) {
-        const float L = sym_llr<MB>(lam + v * MB, x);
-        const uint32_t vp = sc.vn[v];
-        const int e0 = vp >> 8, e1 = e0 + (vp & 255);
-        for (int e = e0; e < e1; ++e) msg[msg_index(Ep, sc.vslot[e], gmul[sc.vh[e] * Q + x])] = L;
-        const int d = group_argmin<Q>(L, x);
-        if (x == 0) dec[v] = (uint8_t)d;
-    }
+    for (int v = tid; v < N; v += nt) vn_lane<Q, MB>(msg, Ep, v, sc, lam, dec, true);
     __syncthreads();
     int fail = syndrome_fail<Q>(g, sc, dec, gmul);
     int it = 0;
@@ -326,19 +320,7 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         }
         __syncthreads();
         // ---- symbol nodes: lane x = variable-domain symbol, reads c2v(x) at position h*x ----
-        for (int v = grp; v < N; v += ngrp) {
-            float app = sym_llr<MB>(lam + v * MB, x);
-            const uint32_t vp = sc.vn[v];
-            const int e0 = vp >> 8, e1 = e0 + (vp & 255);
-            for (int e = e0; e < e1; ++e) app += msg[msg_index(Ep, sc.vslot[e], gmul[sc.vh[e] * Q + x])];
-            const int d = group_argmin<Q>(app, x);
-            if (x == 0) dec[v] = (uint8_t)d;
-            for (int e = e0; e < e1; ++e) {
-                float *p = msg + msg_index(Ep, sc.vslot[e], gmul[sc.vh[e] * Q + x]);
-                const float t = app - *p;
-                *p = t - group_min<Q>(t);
-            }
-        }
+        for (int v = tid; v < N; v += nt) vn_lane<Q, MB>(msg, Ep, v, sc, lam, dec, false);
         __syncthreads();
         fail = syndrome_fail<Q>(g, sc, dec, gmul);
         ++it;
