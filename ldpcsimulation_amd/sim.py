@@ -69,16 +69,19 @@ def stop_reached(bit_err: int, frame_err: int, min_bit_err: int = 200, min_frame
     return not (bit_err < min_bit_err or frame_err < min_frame_err)
 
 
-def exact_cut(prev: np.ndarray, frames: np.ndarray, T: int, min_bit_err=200, min_frame_err=40):
+def exact_cut(prev: np.ndarray, frames: np.ndarray, T: int, min_bit_err=200, min_frame_err=40,
+              iters_in_frames: bool = False):
     """Apply the stop rule frame by frame. prev = counters before this round;
     frames = this round's per-frame results in global frame order. Returns
-    (counters after the last frame the reference would decode, frames used)."""
+    (counters after the last frame the reference would decode, frames used).
+    iters_in_frames: decoders with early stop (GDBF, EMS) report each frame's
+    iterations in its 4th field; otherwise every frame ran T."""
     acc = prev.copy()
     used = 0
-    for w, unc, syn, _ in frames:
+    for w, unc, syn, its in frames:
         if stop_reached(acc[0], acc[1], min_bit_err, min_frame_err):
             break
-        acc += (w, 1 if w > 0 else 0, unc, 1, T, syn)
+        acc += (w, 1 if w > 0 else 0, unc, 1, its if iters_in_frames else T, syn)
         used += 1
     return acc, used
 
@@ -124,7 +127,8 @@ class _Comm:
 
 def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, ebn0_db: float,
                    batch: int, min_bit_err: int = 200, min_frame_err: int = 40,
-                   max_frames: Optional[int] = None, exact_stop: bool = True, device=None) -> PointResult:
+                   max_frames: Optional[int] = None, exact_stop: bool = True, device=None,
+                   iters_in_frames: bool = False) -> PointResult:
     """Run one SNR point to the reference's stop rule.
 
     run_batch(first_cw, n) must decode global frames first_cw..first_cw+n-1 on
@@ -143,7 +147,7 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
         fr = np.ascontiguousarray(run_batch(first, batch))
         raw = fr.view(np.int32).reshape(-1, 4)
         local = np.array([raw[:, 0].sum(), (raw[:, 0] > 0).sum(), raw[:, 1].sum(), len(raw),
-                          T * len(raw), raw[:, 2].sum()], dtype=np.int64)
+                          raw[:, 3].sum() if iters_in_frames else T * len(raw), raw[:, 2].sum()], dtype=np.int64)
         tot = comm.allreduce_sum(local)
         after = acc + tot
         crossed = stop_reached(after[0], after[1], min_bit_err, min_frame_err)
@@ -152,7 +156,7 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
             allf = comm.allgather(raw).reshape(-1, 4)
             if limit_hit:
                 allf = allf[: max(0, max_frames - int(acc[3]))]
-            acc, used = exact_cut(acc, allf, T, min_bit_err, min_frame_err)
+            acc, used = exact_cut(acc, allf, T, min_bit_err, min_frame_err, iters_in_frames)
             w = allf[:used, 0]
             np.add.at(hist_cut, w[w > 0] - 1, 1)
         else:

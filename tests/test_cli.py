@@ -105,3 +105,24 @@ def test_sweep_driver_log_lines(tmp_path):
     assert f[0] == "1" and f[4] == "50" and f[5] == "1.25" and f[6].endswith("80211n_1944_r12.alist")
     fer = [float(l.split("\t")[3]) for l in lines]
     assert 0.25 < fer[0] < 0.6 and 0.005 < fer[1] < 0.04     # SURVEY §6 reference FER 0.417 / 0.0181
+
+
+def test_sweep_driver_bp_and_ems(tmp_path):
+    """sweep --variant bp (decodeBP's log line: SNR BER avgIt FER T alist) and --ems
+    (config 5: SNR BER avgIt FER T nm offset alist, avgIt < T with early stop)."""
+    import sys
+    log = tmp_path / "bp.txt"
+    p = subprocess.run([sys.executable, "-m", "ldpcsimulation_amd.sweep", code_path("PEGReg504x1008.alist"),
+                        "--rate", "0.5", "--snr", "2.0", "-T", "20", "--variant", "bp", "--batch", "4096",
+                        "--seed", "3", "--log", str(log)], cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr
+    f = log.read_text().split("\t")
+    assert len(f) == 6 and f[0] == "2" and f[4] == "20" and 0 < float(f[3]) < 0.2
+    log = tmp_path / "ems.txt"
+    p = subprocess.run([sys.executable, "-m", "ldpcsimulation_amd.sweep", code_path("gf16_N1000_dv2_dc4.alist"),
+                        "--ems", "--rate", "0.5", "--snr", "1.8", "-T", "20", "--batch", "4096", "--seed", "3",
+                        "--log", str(log), "--json"], cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr
+    f = log.read_text().split("\t")
+    assert len(f) == 8 and f[0] == "1.8" and f[4] == "20" and f[5] == "16" and float(f[2]) < 20
+    assert 0 < float(f[3]) < 0.3

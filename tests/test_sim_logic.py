@@ -111,3 +111,22 @@ def test_two_ranks_gloo_identical_to_sequential(batch):
     for rank, counts, h, rounds in out:
         assert counts == want, rank
         assert np.array_equal(np.array(h), hist)
+
+
+def fake_frames_early_stop(first, n):
+    """As fake_frames, with a per-frame iteration count (early-stopping decoders: GDBF, EMS)."""
+    out = fake_frames(first, n)
+    f = np.arange(first, first + n, dtype=np.int64)
+    out["iters"] = np.where(out["bit_err"] > 0, T, 1 + (f * 40503) % 17)
+    return out
+
+
+@pytest.mark.parametrize("batch", [1, 64, 5000])
+def test_exact_stop_counts_reported_iterations(batch):
+    """iters_in_frames: avgIt is the sum of the frames' own iteration counts up to the exact stop."""
+    want, _ = sequential()
+    frames = fake_frames_early_stop(0, want["frames"])
+    res = sim.simulate_point(fake_frames_early_stop, N, T, 1.5, batch, iters_in_frames=True)
+    assert res.counts["frames"] == want["frames"] and res.counts["bit_err"] == want["bit_err"]
+    assert res.counts["iters"] == int(frames["iters"].sum())
+    assert res.avg_iters < T
