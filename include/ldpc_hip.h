@@ -298,7 +298,7 @@ int  ldpc_nb_graph_load_alist(const char *path, ldpc_nb_graph **out);
 int  ldpc_nb_graph_info(const ldpc_nb_graph *g, int *N, int *M, int *q, int *E, int *maxdv, int *maxdc);
 void ldpc_nb_graph_destroy(ldpc_nb_graph *g);
 
-/* Device context (GF(16), row degree <= 16). */
+/* Device context (GF(16), row degree <= 8). */
 int  ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_nb_ctx **out);
 int  ldpc_nb_ctx_set_stream(ldpc_nb_ctx *ctx, void *hip_stream);
 void ldpc_nb_ctx_destroy(ldpc_nb_ctx *ctx);

@@ -136,9 +136,10 @@ __device__ __forceinline__ void store_out(float *msg, int Ep, int slot, float (&
 // operands, each sum being one commutative add). Each lane writes the
 // outputs of its half: own positions lo .. D-1, lo = ceil(D/2) / floor(D/2).
 // In place and race-free: the two lanes run the same instruction stream in
-// lockstep, and a re-read of an input (own position kp, kp > (D-1)/2) never
-// meets a position the partner lane has already written (positions >= kp of
-// its own order, i.e. <= D-1-kp < kp of ours).
+// lockstep; a re-read of an input (own position kp, kp >= lo + 1 > (D-2)/2)
+// comes before this lane's own store to kp and never meets a position the
+// partner lane has already written (its positions > kp of its own order,
+// i.e. original positions <= D-2-kp < kp of ours).
 template <int Q, int D>
 __device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int dir, int nm, float offset)
 {
@@ -162,14 +163,17 @@ __device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int di
         if (kp >= lo) {
             ecn_reg<Q>(F[kp - 1], B, W);
             trunc_vec<Q>(W, nm);
-            store_out<Q>(msg, Ep, slot(kp), W, nm, offset);
-            if (kp - 1 >= lo) {
+            if (kp - 1 >= lo) {   // next backward step: read input kp BEFORE this lane overwrites it
+                float Bn[Q];
                 load_vec<Q>(msg, Ep, slot(kp), U);
                 trunc_vec<Q>(U, nm);
-                ecn_reg<Q>(B, U, W);
-                trunc_vec<Q>(W, nm);
+                ecn_reg<Q>(B, U, Bn);
+                trunc_vec<Q>(Bn, nm);
+                store_out<Q>(msg, Ep, slot(kp), W, nm, offset);
 #pragma unroll
-                for (int x = 0; x < Q; ++x) B[x] = W[x];
+                for (int x = 0; x < Q; ++x) B[x] = Bn[x];
+            } else {
+                store_out<Q>(msg, Ep, slot(kp), W, nm, offset);
             }
         }
     }

@@ -231,3 +231,27 @@ def test_ems_waterfall(nbctx):
         assert ((fr["iters"] < 30) <= (fr["syndrome_fail"] == 0)).all()
         fer.append(cnt.frame_err / cnt.frames)
     assert fer[0] > fer[1] > fer[2] and fer[0] > 0.5 and fer[2] < 0.05, fer
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2000, 1000, 2), (400, 200, 4), (300, 200, 3)],
+                         ids=["global_state_N2000", "dc8_kernel", "irregular_dc"])
+def test_ems_other_kernels_bit_exact(shape):
+    """The global-memory message slot (codes beyond LDS), the DC=8 build (row degree 5..8)
+    and irregular row degrees, against the oracle."""
+    native = _native()
+    codes = _codes()
+    N, M, dv = shape
+    H = codes.peg_nb_code(N, M, dv, 16, seed=N + M)
+    g = native.NbGraph.from_lists(H.N, H.M, H.q, H.cols, H.rows)
+    ctx = native.NbContext(g, 0, 64)
+    info = ctx.kernel_info()
+    assert info["kernel"] == ("ems_global" if N == 2000 else "ems_lds")
+    A = O.NbCode(H)
+    y, n0 = _frames(H.N * 4, 6, 2.2, seed=N)
+    for c in (dict(nm=16, offset=0.0, early_stop=True), dict(nm=6, offset=0.5, early_stop=False)):
+        for T in (1, 8):
+            d, fr, _ = ctx.decode(y, n0, native.EmsConfig(T=T, **c))
+            want, its, sf = A.decode(y, n0, T, **c)
+            assert int((d != want).sum()) == 0, (c, T)
+            assert np.array_equal(fr["iters"], its) and np.array_equal(fr["syndrome_fail"], sf)
