@@ -26,7 +26,7 @@ __device__ __forceinline__ float bp_log(float x) { return logf(x); }
 __device__ __forceinline__ double bp_log(double x) { return log(x); }
 template <typename F> __device__ __forceinline__ F bp_abs(F x) { return x < F(0) ? -x : x; }
 
-template <typename F, int SRC>
+template <typename F, int SRC, int DCB>
 __device__ __forceinline__ void bp_codeword(const DecodeArgs &a, const DevGraph &g, int b, F *app, F *yq, F *c2v,
                                             int *red)
 {
@@ -85,22 +85,28 @@ __device__ __forceinline__ void bp_codeword(const DecodeArgs &a, const DevGraph 
             const int deg = g.row_deg[j];
             const int32_t *rc = g.row_cols + (size_t)j * dcs;
             F *cj = c2v + (size_t)j * dcs;
-            F th[kBpMaxDc];
-            for (int k = 0; k < deg; ++k) {
-                F v = app[rc[k]] - cj[k];                                  // v2c = sum - c2v (:399)
-                if (bp_abs(v) > maxllr) v = maxllr * (v >= F(0) ? F(1) : F(-1));   // :400-401
-                th[k] = bp_tanh(v / F(2));
-            }
-            for (int jj = 0; jj < deg; ++jj) {
-                F prod = F(1);
-                for (int k = 0; k < deg; ++k)
-                    if (k != jj) prod *= th[k];
-                F o = bp_log((F(1) + prod) / (F(1) - prod));
-                // fp32: tanhf(10) rounds to 1 and 1 - prod to 0; clip c2v to
-                // +-MAXLLR (a no-op in exact arithmetic, see oracle/bp_oracle.c)
-                if (sizeof(F) == 4 && bp_abs(o) > maxllr) o = o >= F(0) ? maxllr : -maxllr;
-                cj[jj] = o;
-            }
+            // DCB >= deg, loops unrolled so that th[] lives in registers
+            F th[DCB];
+#pragma unroll
+            for (int k = 0; k < DCB; ++k)
+                if (k < deg) {
+                    F v = app[rc[k]] - cj[k];                              // v2c = sum - c2v (:399)
+                    if (bp_abs(v) > maxllr) v = maxllr * (v >= F(0) ? F(1) : F(-1));   // :400-401
+                    th[k] = bp_tanh(v / F(2));
+                }
+#pragma unroll
+            for (int jj = 0; jj < DCB; ++jj)
+                if (jj < deg) {
+                    F prod = F(1);
+#pragma unroll
+                    for (int k = 0; k < DCB; ++k)
+                        if (k != jj && k < deg) prod *= th[k];
+                    F o = bp_log((F(1) + prod) / (F(1) - prod));
+                    // fp32: tanhf(10) rounds to 1 and 1 - prod to 0; clip c2v to
+                    // +-MAXLLR (a no-op in exact arithmetic, see oracle/bp_oracle.c)
+                    if (sizeof(F) == 4 && bp_abs(o) > maxllr) o = o >= F(0) ? maxllr : -maxllr;
+                    cj[jj] = o;
+                }
         }
         __syncthreads();
         // ---- bit nodes: sum in nlist order (:384-393) ----
@@ -155,22 +161,22 @@ static size_t bp_state_bytes(const DevGraph &g, size_t fsz)
     return (fsz * (2 * (size_t)g.N + (size_t)g.M * g.dcs) + 255) & ~(size_t)255;
 }
 
-template <typename F, int SRC>
+template <typename F, int SRC, int DCB>
 __global__ __launch_bounds__(512) void k_bp_lds(DecodeArgs a, DevGraph g)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int red[16 * 4];
     F *app = reinterpret_cast<F *>(smem);
-    bp_codeword<F, SRC>(a, g, blockIdx.x, app, app + g.N, app + 2 * g.N, red);
+    bp_codeword<F, SRC, DCB>(a, g, blockIdx.x, app, app + g.N, app + 2 * g.N, red);
 }
 
-template <typename F, int SRC>
+template <typename F, int SRC, int DCB>
 __global__ __launch_bounds__(512) void k_bp_global(DecodeArgs a, DevGraph g, unsigned char *scratch, size_t slot)
 {
     __shared__ int red[16 * 4];
     F *app = reinterpret_cast<F *>(scratch + slot * blockIdx.x);
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
-        bp_codeword<F, SRC>(a, g, b, app, app + g.N, app + 2 * g.N, red);
+        bp_codeword<F, SRC, DCB>(a, g, b, app, app + g.N, app + 2 * g.N, red);
 }
 
 constexpr size_t kBpMaxLds = 160 * 1024;
@@ -193,12 +199,12 @@ KernelChoice bp_choose(const DevGraph &g, bool f64)
     return kc;
 }
 
-template <typename F, int SRC>
-static hipError_t bp_launch_t(const DevGraph &g, const DecodeArgs &a, const KernelChoice &kc, void *gs, int gblocks,
+template <typename F, int SRC, int DCB>
+static hipError_t bp_launch_d(const DevGraph &g, const DecodeArgs &a, const KernelChoice &kc, void *gs, int gblocks,
                               hipStream_t s)
 {
     if (kc.lds_bytes > 0) {
-        auto fn = k_bp_lds<F, SRC>;
+        auto fn = k_bp_lds<F, SRC, DCB>;
         if (kc.lds_bytes > 64 * 1024) {
             hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                kc.lds_bytes);
@@ -208,10 +214,19 @@ static hipError_t bp_launch_t(const DevGraph &g, const DecodeArgs &a, const Kern
     } else {
         const int grid = gblocks < a.batch ? gblocks : a.batch;
         if (grid <= 0 || !gs) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_bp_global<F, SRC>), dim3(grid), dim3(kc.threads), 0, s, a, g, (unsigned char *)gs,
+        hipLaunchKernelGGL((k_bp_global<F, SRC, DCB>), dim3(grid), dim3(kc.threads), 0, s, a, g, (unsigned char *)gs,
                            kc.scratch_per_block);
     }
     return hipGetLastError();
+}
+
+template <typename F, int SRC>
+static hipError_t bp_launch_t(const DevGraph &g, const DecodeArgs &a, const KernelChoice &kc, void *gs, int gblocks,
+                              hipStream_t s)
+{
+    if (g.dcs <= 8) return bp_launch_d<F, SRC, 8>(g, a, kc, gs, gblocks, s);
+    if (g.dcs <= 16) return bp_launch_d<F, SRC, 16>(g, a, kc, gs, gblocks, s);
+    return bp_launch_d<F, SRC, kBpMaxDc>(g, a, kc, gs, gblocks, s);
 }
 
 hipError_t bp_launch(const DevGraph &g, const DecodeArgs &a, bool f64, const KernelChoice &kc, void *gscratch,
