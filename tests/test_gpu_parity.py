@@ -233,16 +233,26 @@ def test_syndrome_and_codeword_mode(gpu_ctx_factory):
 
 def test_fer_matches_reference_statistically(gpu_ctx_factory):
     """802.11n N=1944 NMS a=1.25 T=50: GPU fp32 Philox FER vs the reference's (REF_SEED=11):
-    two-proportion z-test |z| < 3 at 1.0/1.25/1.5 dB."""
+    two-proportion z-test |z| < 3 at all four SURVEY §8(d) points, 1.0/1.25/1.5/1.75 dB.
+    1.75 dB (reference 40/41745) decodes 8 x 16384 frames so the GPU side holds
+    ~100+ frame errors (collect >= 100 on the GPU)."""
     native = _native()
     from ldpcsimulation_amd.sim import two_proportion_z
     ctx = gpu_ctx_factory("80211n_1944_r12.alist", 16384)
     cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50)
-    ref = {1.0: (40, 96), 1.25: (40, 362), 1.5: (40, 2212)}
-    for ebn0, (k_ref, n_ref) in ref.items():
-        _, cnt = ctx.sim_batch(ebn0, 0.5, cfg, seed=2026, stream_id=int(ebn0 * 100), first_cw=0, batch=16384)
-        z = two_proportion_z(cnt.frame_err, cnt.frames, k_ref, n_ref)
-        assert abs(z) < 3, (ebn0, cnt.frame_err, cnt.frames, z)
+    ref = {1.0: (40, 96, 1), 1.25: (40, 362, 1), 1.5: (40, 2212, 1), 1.75: (40, 41745, 8)}
+    for ebn0, (k_ref, n_ref, rounds) in ref.items():
+        ferr = frames = 0
+        for r in range(rounds):
+            _, cnt = ctx.sim_batch(ebn0, 0.5, cfg, seed=2026, stream_id=int(ebn0 * 100), first_cw=r * 16384,
+                                   batch=16384, want_frames=False)
+            ferr += cnt.frame_err
+            frames += cnt.frames
+        assert frames == rounds * 16384
+        z = two_proportion_z(ferr, frames, k_ref, n_ref)
+        assert abs(z) < 3, (ebn0, ferr, frames, z)
+        if rounds > 1:
+            assert ferr >= 60, (ebn0, ferr, frames)
 
 
 @pytest.mark.parametrize("prec", ["f32", "f64"])
