@@ -174,8 +174,11 @@ def ensure_80211n_1944() -> str:
     path = os.path.join(codes_dir(), "80211n_1944_r12.alist")
     txt = alist_text(ieee80211n_r12(81))
     if not os.path.exists(path) or open(path).read() != txt:
-        with open(path, "w") as f:
+        # write-then-rename: ranks of a multi-GPU run may get here together
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
             f.write(txt)
+        os.replace(tmp, path)
     return path
 
 
