@@ -95,8 +95,21 @@ def cpu_baseline(alist: str, T: int, alpha: float, procs: int) -> dict:
                              env=dict(os.environ, REF_SEED="7"), capture_output=True, text=True, check=True).stdout
     t_one = time.perf_counter() - t1
     f_one = int([l for l in out.splitlines() if l.startswith("Final result:")][0].split(" words")[0].split()[-1])
+    # the same run built with the reference Makefile's own flags (-g, no -O): the "as shipped" rate
+    single_g = None
+    ref_g = os.path.join(ROOT, "oracle", "_ref", "decodeNMS_g")
+    if os.path.exists(ref_g):
+        t2 = time.perf_counter()
+        with tempfile.TemporaryDirectory() as td:
+            out = subprocess.run([ref_g, alist, "0.5", "0.0", str(T), str(alpha), f"{td}/l.txt"],
+                                 env=dict(os.environ, REF_SEED="7"), capture_output=True, text=True,
+                                 check=True).stdout
+        t_g = time.perf_counter() - t2
+        f_g = int([l for l in out.splitlines() if l.startswith("Final result:")][0].split(" words")[0].split()[-1])
+        single_g = f_g * N / t_g / 1e6
     return {"value": frames * N / wall / 1e6, "unit": "Mbit/s", "cores": procs, "kind": kind,
             "single_core_mbit_s": f_one * N / t_one / 1e6,
+            "single_core_mbit_s_as_shipped_O0_g": single_g,
             "cpu_model": _cpu_model(),
             "sample": f"{procs} processes x {runs_per_proc} runs of oracle/_ref/decodeNMS (unmodified reference, g++ -O2), "
                       f"802.11n N=1944 NMS alpha={alpha} T={T}, 0.0 dB (stop rule ends each run at 40 frames); "
