@@ -521,6 +521,8 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
             int want = 1;
             if (const char *e = std::getenv("LDPC_LAYERED_BPC")) want = std::max(1, std::atoi(e));
             per_cu = std::min(per_cu, want);
+        } else if (const char *e = std::getenv("LDPC_FLOOD_BPC")) {   // global flooding kernel (experiments)
+            per_cu = std::min(per_cu, std::max(1, std::atoi(e)));
         }
         if (per_cu <= 0) per_cu = 1;
         gblocks = per_cu * c->num_cus;

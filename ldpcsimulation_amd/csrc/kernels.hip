@@ -324,7 +324,7 @@ template <> struct F2T<float> { using T = float2; };
 template <> struct F2T<double> { using T = double2; };
 
 template <typename F, int SRC, int DC>
-__global__ __launch_bounds__(512, 4) void k_decode_flood(DecodeArgs a, DevGraph g, FloodSched fs, unsigned char *scratch,
+__global__ __launch_bounds__(512, (sizeof(F) == 4 && DC <= 8) ? 8 : 4) void k_decode_flood(DecodeArgs a, DevGraph g, FloodSched fs, unsigned char *scratch,
                                                       size_t slot_bytes)
 {
     using F2 = typename F2T<F>::T;
