@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 5
+#define LDPC_ABI_VERSION 6
 
 typedef enum {
     LDPC_OK = 0,
@@ -208,6 +208,12 @@ int  ldpc_ctx_last_kernel_ms(ldpc_ctx *ctx, float *ms);
  * forces the global-memory kernel, for testing it on small codes. */
 int  ldpc_ctx_kernel_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, char *name, int name_len,
                           int *lds_bytes, int *blocks_per_cu);
+/* Codewords of the last min-sum launch that the fast row kernel (fp64,
+ * "rows_fast") handed to the exact path because its premise failed (huge or
+ * non-finite values, minima below 2^-960; 0 for any launch that did not use
+ * the fast kernel). Diagnostic of the fast/exact split; synchronises the
+ * stream. No reference counterpart (the reference has one exact path). */
+int  ldpc_ctx_redo_count(ldpc_ctx *ctx, int64_t *n);
 
 /* ---- GDBF / NGDBF bit flipping (BASELINE config 4) --------------------- */
 /* src/decodeGDBF.cpp in its parallel-flip mode (mu = 1): syndrome check

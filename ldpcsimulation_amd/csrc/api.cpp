@@ -90,6 +90,8 @@ struct ldpc_ctx {
     ldpc::LayerSched ls{};                                // layered schedule (row order = fs order)
     DevBuf lsched;
     DevBuf divcheck;                                      // mismatch counter of verify_div_by_reciprocal
+    DevBuf redo;                                          // re-decode list of the fast row kernel
+    bool last_fast = false;                               // last min-sum launch used the fast row kernel
     std::vector<std::pair<float, bool>> div_ok;           // alpha -> reciprocal division exact
 };
 
@@ -206,7 +208,8 @@ static void ctx_free(ldpc_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->graph, &c->counts, &c->hist, &c->y_stage, &c->c_stage, &c->d_stage, &c->fw_stage,
-                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck, &c->fsched, &c->lsched, &c->p_stage})
+                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck, &c->fsched, &c->lsched, &c->p_stage,
+                      &c->redo})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -494,6 +497,16 @@ static ldpc::KernelChoice select_kernel(const ldpc_ctx *c, bool f64, int schedul
 
 static bool is_layered(const ldpc::KernelChoice &kc) { return kc.name[0] == 'l' && kc.name[1] == 'a'; }
 
+// fp64 row graphs run the fast-path row kernel (rows_fast.hip) plus the exact
+// re-decode of codewords whose premise failed; LDPC_ROWS=old keeps the old one.
+static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64)
+{
+    const char *env = std::getenv("LDPC_ROWS");
+    if (env && std::strcmp(env, "old") == 0) return false;
+    return kc.name[0] == 'r' && c->has_rs && ldpc::rows_fast_supported(c->rs, f64) &&
+           ldpc::redo_lds_bytes(c->dg, f64) <= 160 * 1024;
+}
+
 static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int schedule)
 {
     const ldpc::KernelChoice kc = select_kernel(c, f64, schedule, a.variant);
@@ -541,8 +554,17 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
     }
 #define a as
 #endif
+    // fp64 row graphs: the fast-path kernel plus the exact re-decode of any
+    // codeword whose premise failed (LDPC_ROWS=old keeps the old row kernel).
+    const bool fast = use_rows_fast(c, kc, f64);
+    if (fast) HIP_TRY(c->redo.ensure(sizeof(unsigned) * ((size_t)c->max_batch + 1)));
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    if (layered)
+    c->last_fast = fast;
+    if (fast) {
+        HIP_TRY(hipMemsetAsync(c->redo.p, 0, sizeof(unsigned), c->stream));
+        HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, kc.lds_bytes, (unsigned *)c->redo.p, c->stream, c->num_cus));
+        HIP_TRY(ldpc::launch_redo(c->dg, a, f64, (const unsigned *)c->redo.p, c->stream, c->num_cus));
+    } else if (layered)
         HIP_TRY(ldpc::launch_layered(c->dg, a, f64, kc, c->fs, c->ls, c->gscratch.p, gblocks, c->stream));
     else
         HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream,
@@ -827,6 +849,19 @@ int ldpc_ctx_last_kernel_ms(ldpc_ctx *c, float *ms)
     return LDPC_OK;
 }
 
+int ldpc_ctx_redo_count(ldpc_ctx *c, int64_t *n)
+{
+    if (!c || !n) return set_err(LDPC_ERR_INVALID, "null argument");
+    *n = 0;
+    if (!c->last_fast || !c->redo.p) return LDPC_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    unsigned h = 0;
+    HIP_TRY(hipMemcpyAsync(&h, c->redo.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *n = (int64_t)h;
+    return LDPC_OK;
+}
+
 int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, int name_len, int *lds_bytes,
                          int *bpc)
 {
@@ -836,7 +871,8 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     int rc = check_cfg(c, cfg);
     if (rc) return rc;
     const ldpc::KernelChoice kc = select_kernel(c, f64, cfg->schedule, cfg->variant);
-    if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", kc.name);
+    if (name && name_len > 0)
+        std::snprintf(name, (size_t)name_len, "%s", cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64) ? "rows_fast" : kc.name);
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
     if (bpc) *bpc = cfg->variant == LDPC_BP ? 0 : is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
                                    : ldpc::blocks_per_cu(c->dg, f64, kc);

@@ -108,6 +108,20 @@ constexpr int kPackedMaxDc = 26;
 // normalisation divides: |v2c| minima). *mismatches receives the count.
 hipError_t verify_div_by_reciprocal(float alpha, float rcp, unsigned long long *mismatches_dev, hipStream_t s);
 
+// Fast-path row kernel (rows_fast.hip): fp64, same LDS layout and schedule as
+// the "rows" kernel (lds_bytes of its KernelChoice), check node compiled per
+// variant; codeword groups whose premise fails are appended to redo
+// (redo[0] = count, must be 0 at launch; redo[1..] batch indices, capacity
+// batch), and launch_redo (kernels.hip) decodes them on the exact path.
+bool rows_fast_supported(const RowSched &rs, bool f64);
+hipError_t launch_rows_fast(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, int lds_bytes,
+                            unsigned *redo, hipStream_t s, int num_cus);
+// alpha for which the fast fp64 NMS division x*r + one fma correction is exact
+bool markstein_exact_alpha(double alpha);
+size_t redo_lds_bytes(const DevGraph &g, bool f64);
+hipError_t launch_redo(const DevGraph &g, const DecodeArgs &a, bool f64, const unsigned *redo, hipStream_t s,
+                       int num_cus);
+
 // Row-kernel template bounds (host picks the smallest that fits).
 constexpr int kRowsMaxThreads = 1024;
 constexpr int kRowsCpt[] = {2, 4, 8};

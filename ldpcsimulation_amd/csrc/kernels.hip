@@ -21,6 +21,7 @@
 // no FMA may fuse the channel's 1 + sigma*n or the quantiser.
 #include "kernels.h"
 #include "device_common.h"
+#include "minsum_common.h"
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -29,55 +30,6 @@
 
 namespace ldpc {
 
-enum { V_MS = 0, V_NMS = 1, V_OMS = 2 };
-
-template <typename F> struct RowState;
-template <> struct __attribute__((aligned(16))) RowState<float> { float m1, m2; uint64_t meta; };
-template <> struct __attribute__((aligned(16))) RowState<double> { double m1, m2; uint64_t meta, pad; };
-
-template <typename F> __device__ __forceinline__ F dinf();
-template <> __device__ __forceinline__ float dinf<float>() { return __builtin_huge_valf(); }
-template <> __device__ __forceinline__ double dinf<double>() { return __builtin_huge_val(); }
-__device__ __forceinline__ float dabs(float x) { return __builtin_fabsf(x); }
-__device__ __forceinline__ double dabs(double x) { return __builtin_fabs(x); }
-__device__ __forceinline__ float dfloor(float x) { return __builtin_floorf(x); }
-// IEEE minNum: a NaN operand yields the other operand.
-__device__ __forceinline__ float dmin(float a, float b) { return __builtin_fminf(a, b); }
-__device__ __forceinline__ double dmin(double a, double b) { return __builtin_fmin(a, b); }
-__device__ __forceinline__ double dfloor(double x) { return __builtin_floor(x); }
-
-// sgn() of the reference (:518-523): x >= 0 -> +1 (so -0.0 -> +1, NaN -> -1).
-template <typename F> __device__ __forceinline__ F dsgn(F x) { return x >= F(0) ? F(1) : F(-1); }
-
-// quantize() (:480-489), same operation order.
-template <typename F>
-__device__ __forceinline__ F quantize(F x, F ymax, F nq)
-{
-    if (dabs(x) > ymax) return dsgn(x) * ymax;
-    F q = dsgn(x) * (dfloor(dabs(x) * (nq - F(1)) / (F(2) * ymax)) + F(0)) * (F(2) * ymax / (nq - F(1)));
-    if (q == F(0)) q = dsgn(x) * F(2) * ymax / (nq - F(1));
-    return q;
-}
-
-template <typename F>
-__device__ __forceinline__ F front_end(F y, const DecodeArgs &a)
-{
-    F q = y;
-    if (a.quantize) q = quantize<F>(y, (F)a.ymax, (F)a.nq);
-    if (a.saturate) {
-        const F ym = (F)a.ymax;
-        if (q > ym) q = ym;
-        if (q < -ym) q = -ym;
-    }
-    return q;
-}
-
-// Diagnostic phase timing (-DLDPC_STAMPS builds only; never in the shipped kernel).
-#ifdef LDPC_STAMPS
-#define STAMP(var) unsigned long long var = (threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0ull
-#else
-#define STAMP(var) [[maybe_unused]] constexpr unsigned long long var = 0ull
-#endif
 
 // ---------------------------------------------------------------------
 // One codeword, all T iterations. rows/app/yq may live in LDS or in a
@@ -242,6 +194,22 @@ __global__ __launch_bounds__(256) void k_decode_lds(DecodeArgs a, DevGraph g)
     decode_codeword<F, SRC>(a, g, blockIdx.x, rows, app, yq, red);
 }
 
+// Re-decode list of the fast row kernel (rows_fast.hip): redo[0] codewords
+// whose fast-path premise failed, batch indices in redo[1..]; each is decoded
+// from scratch on this exact path (state in LDS), persistent grid. With an
+// empty list every block exits at once.
+template <typename F, int SRC>
+__global__ __launch_bounds__(256) void k_redo(DecodeArgs a, DevGraph g, const unsigned *redo)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    RowState<F> *rows = reinterpret_cast<RowState<F> *>(smem);
+    F *app = reinterpret_cast<F *>(smem + sizeof(RowState<F>) * (size_t)g.M);
+    F *yq = app + g.N;
+    int *red = reinterpret_cast<int *>(yq + g.N);
+    const unsigned n = redo[0];
+    for (unsigned i = blockIdx.x; i < n; i += gridDim.x) decode_codeword<F, SRC>(a, g, (int)redo[1 + i], rows, app, yq, red);
+}
+
 // State in a global scratch slot per workgroup (codes whose state exceeds
 // LDS, e.g. DVB-S2 N=64800): persistent grid, codewords strided.
 template <typename F, int SRC>
@@ -272,19 +240,6 @@ __global__ __launch_bounds__(256) void k_decode_global(DecodeArgs a, DevGraph g,
 // normalise/offset, scatter the new c2v) | barrier | bit phase (sum yq + c2v
 // in nlist order, write app) | barrier.
 // =====================================================================
-template <int DC> struct MetaOf { using T = uint32_t; static constexpr int SH = 5; };
-template <> struct MetaOf<32> { using T = uint64_t; static constexpr int SH = 6; };
-
-template <int DC>
-__device__ __forceinline__ int u16_at(const uint32_t (&w)[DC / 2], int k)
-{
-    return (int)((w[k >> 1] >> ((k & 1) * 16)) & 0xffffu);
-}
-
-// The C codewords of a block are interleaved in LDS: one Pack = the same
-// element of all C codewords, so every gather/scatter moves C values
-// (ds_read_b64 / ds_write_b64 for two fp32 codewords or one fp64).
-template <typename F, int C> struct __attribute__((aligned(sizeof(F) * C))) Pack { F v[C]; };
 
 // x / alpha for the check-node normalisation (:498). fp32 with a verified
 // alpha: reciprocal + one FMA correction (3 VALU instead of ~10); otherwise,
@@ -786,60 +741,6 @@ __global__ __launch_bounds__(512) void k_decode_layered_global(DecodeArgs a, Dev
     flush_acc(a, acc);
 }
 
-// s += r for every codeword of a pack (one v_pk_add_f32 for two fp32 codewords).
-template <typename F, int C>
-__device__ __forceinline__ void padd(Pack<F, C> &s, const Pack<F, C> &r)
-{
-#pragma unroll
-    for (int c = 0; c < C; ++c) s.v[c] += r.v[c];
-}
-template <>
-__device__ __forceinline__ void padd<float, 2>(Pack<float, 2> &s, const Pack<float, 2> &r)
-{
-    using V = float __attribute__((ext_vector_type(2)));
-    V a, b;
-    __builtin_memcpy(&a, &s, sizeof(V));
-    __builtin_memcpy(&b, &r, sizeof(V));
-    a += b;
-    __builtin_memcpy(&s, &a, sizeof(V));
-}
-
-// Bit nodes, edges k in [k, kend) of the first NACT slots (every one of them has
-// group degree >= kend): sum_i += c2v[base_i + k*64] (c2v already offset by the
-// lane, base_i wave-uniform), in edge order per slot, U edges of every slot in
-// flight per step. (Steps sized exactly to the remainder were measured slower:
-// the extra unrolled variants cost more in instruction fetch than they save.)
-template <typename F, int C, int NACT, int CPT>
-__device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base)[CPT], int &k, int kend,
-                                         Pack<F, C> (&sum)[CPT])
-{
-    constexpr int U = NACT >= 3 ? 2 : 4;   // at most 8 packs in flight
-    for (; k + U <= kend; k += U) {
-        Pack<F, C> r[NACT][U];
-#pragma unroll
-        for (int i = 0; i < NACT; ++i)
-#pragma unroll
-            for (int u = 0; u < U; ++u) r[i][u] = c2v[base[i] + (k + u) * 64];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int i = 0; i < NACT; ++i) padd(sum[i], r[i][u]);
-    }
-    for (; k < kend; ++k) {
-        Pack<F, C> r[NACT];
-#pragma unroll
-        for (int i = 0; i < NACT; ++i) r[i] = c2v[base[i] + k * 64];
-#pragma unroll
-        for (int i = 0; i < NACT; ++i) padd(sum[i], r[i]);
-    }
-}
-template <typename F, int C, int NACT, int CPT>
-__device__ __forceinline__ void vn_phases(const Pack<F, C> *c2v, const int (&base)[CPT], const int (&gd)[CPT], int &k,
-                                          Pack<F, C> (&sum)[CPT])
-{
-    vn_phase<F, C, NACT, CPT>(c2v, base, k, gd[NACT - 1], sum);
-    if constexpr (NACT > 1) vn_phases<F, C, NACT - 1, CPT>(c2v, base, gd, k, sum);
-}
 
 // Check node, exact path: the reference's comparisons for any input, incl.
 // infinities and NaN (checkNodeUpdates :410-450, applyNormalization :494-499,
@@ -1427,6 +1328,24 @@ static hipError_t launch_t(const DevGraph &g, const DecodeArgs &a, const KernelC
                            (unsigned char *)gs, kc.scratch_per_block);
     }
     return hipGetLastError();
+}
+
+size_t redo_lds_bytes(const DevGraph &g, bool f64) { return (state_bytes(g, f64) + 64 + 15) & ~(size_t)15; }
+
+hipError_t launch_redo(const DevGraph &g, const DecodeArgs &a, bool f64, const unsigned *redo, hipStream_t s,
+                       int num_cus)
+{
+    const size_t lds = redo_lds_bytes(g, f64);
+    auto go = [&](auto fn) -> hipError_t {
+        if (lds > 64 * 1024) {
+            hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return e;
+        }
+        hipLaunchKernelGGL(fn, dim3(num_cus), dim3(kThreads), lds, s, a, g, redo);
+        return hipGetLastError();
+    };
+    if (f64) return a.src == SRC_GIVEN ? go(k_redo<double, SRC_GIVEN>) : go(k_redo<double, SRC_PHILOX>);
+    return a.src == SRC_GIVEN ? go(k_redo<float, SRC_GIVEN>) : go(k_redo<float, SRC_PHILOX>);
 }
 
 // Row kernel: dispatch on (C, DC, CPT). Persistent grid of the resident blocks.

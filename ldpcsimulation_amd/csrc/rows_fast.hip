@@ -1,0 +1,466 @@
+// rows_fast.hip -- the fast-path row kernel (throughput path of the flooding
+// min-sum decoder, src/decodeMinSum.cpp:247-263), fp64 first.
+//
+// Dataflow (same as kernels.hip's k_decode_rows): a 512-thread
+// workgroup decodes C codewords at once for all T iterations with its whole
+// state in LDS -- app[N+2] posteriors and the c2v messages in bit-slot-major
+// order (a wave's bit-node reads are 64 consecutive words). Thread t owns
+// check rows t and t+512 (RPT = 2) with their bit indices / c2v slots and
+// the c2v it sent last iteration in registers, and up to CPT bit slots.
+//
+// What differs: the kernel holds ONLY the fast check node, compiled per
+// variant (MS / NMS / OMS) and division mode, so nothing of the exact path
+// or of the other variants competes for registers (the old fp64 instance
+// spilled 105 VGPRs to scratch, gather addresses included: 75 ms per
+// 65 536-codeword launch). Its premise (below) is checked on every row; a
+// codeword group that breaks it is abandoned and appended to a re-decode
+// list, which k_redo (kernels.hip: the exact one-codeword-per-block path)
+// decodes right after, in the same stream. Results are therefore identical
+// to the exact kernels for every input; the re-decode list is empty for any
+// sane channel (fp64: it needs |c2v| >= 2^1000 or minima below 2^-960).
+//
+// fp64 fast check node (checkNodeUpdates :410-450, applyNormalization
+// :494-499, applyOffset :503-515). Premise: every app and c2v entering the
+// iteration is finite with magnitude < 2^1000 (so |v2c| < 2^1009: no inf,
+// no NaN) and app is never -0 (yq is canonicalised with + 0.0; a sum that
+// starts at +0 and never adds two -0s cannot be -0, and app - c2v is -0
+// only when app is -0). Then
+//  * sgn(v2c) (:518-523) is the sign bit of v2c's high word, the row's
+//    product of signs is the xor of those words (v_bitop3 0x96), and each
+//    output's sign is parity ^ sign(v2c_k) (v_bitop3 0x78) -- also for a
+//    +0 magnitude, as prod*min*sgn gives;
+//  * (min1, min2) = the two smallest |v2c| of the multiset, by a min/max
+//    tournament (20 v_min/max_f64 for 8 edges): exactly what the
+//    reference's `<=` / `<` update yields for non-NaN inputs;
+//  * the argmin edge is recognised as |v2c_k| == min1 (on a tie min2 ==
+//    min1, so which tied edge the reference picked does not matter);
+//  * x / alpha (NMS) is IEEE division, or, for alpha = P * 2^E with an odd
+//    P < 2^20 (1.25 = 5/4), Markstein's q = x*r, q += fma(-q, alpha, x)*r
+//    with r = RN(1/alpha): q is within 1.5 ulp of x/alpha, the remainder
+//    x - q*alpha is exact (it needs <= 22 bits), the corrected value is
+//    x/alpha + d with |d| <= 1.5 ulp * 2^-53, and x/alpha, a fraction of
+//    denominator P in units of the result's ulp, is at least 1/(2P) ulp
+//    away from every rounding midpoint -- so the correction rounds to
+//    RN(x/alpha). Valid for 2^-960 <= x < 2^1000 and x = 0;
+//    other minima break the premise.
+// fp32 (C = 2 codewords per block) uses cn_fast of minsum_common.h.
+#include "kernels.h"
+#include "device_common.h"
+#include "minsum_common.h"
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdlib>
+
+namespace ldpc {
+
+#ifndef LDPC_FAST_PREFETCH
+#define LDPC_FAST_PREFETCH 1
+#endif
+
+constexpr double kFast64Max = 0x1p1000;    // premise bound on |yq| and |c2v|
+constexpr double kFast64Tiny = 0x1p-960;   // Markstein division: minima >= this (or 0)
+
+__device__ __forceinline__ uint32_t hi32(double d) { return (uint32_t)((unsigned long long)__double_as_longlong(d) >> 32); }
+__device__ __forceinline__ uint32_t lo32(double d) { return (uint32_t)(unsigned long long)__double_as_longlong(d); }
+__device__ __forceinline__ double mkd(uint32_t lo, uint32_t hi)
+{
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// (m1, m2) = the two smallest of |x[K0..K0+N)| by a min/max tournament.
+template <int K0, int N, int DC>
+__device__ __forceinline__ void two_min(const double (&x)[DC], double &m1, double &m2)
+{
+    if constexpr (N == 1) {
+        m1 = __builtin_fabs(x[K0]);
+        m2 = __builtin_huge_val();
+    } else if constexpr (N == 2) {
+        m1 = __builtin_fmin(__builtin_fabs(x[K0]), __builtin_fabs(x[K0 + 1]));
+        m2 = __builtin_fmax(__builtin_fabs(x[K0]), __builtin_fabs(x[K0 + 1]));
+    } else {
+        constexpr int L = N / 2;
+        double l1, l2, r1, r2;
+        two_min<K0, L, DC>(x, l1, l2);
+        two_min<K0 + L, N - L, DC>(x, r1, r2);
+        m1 = __builtin_fmin(l1, r1);
+        m2 = __builtin_fmin(__builtin_fmax(l1, r1), __builtin_fmin(l2, r2));
+    }
+}
+
+template <int VAR, bool FDIV>
+__device__ __forceinline__ double norm64(double m, double alpha, double rcp, double delta)
+{
+    if constexpr (VAR == V_NMS) {
+        if constexpr (FDIV) {
+            const double q = m * rcp;
+            return __builtin_fma(__builtin_fma(-q, alpha, m), rcp, q);
+        } else {
+            return m / alpha;                                       // :498 (IEEE division)
+        }
+    } else if constexpr (VAR == V_OMS) {
+        const double t = m - delta;                                 // :509
+        return t > 0.0 ? t : 0.0;                                   // :513
+    } else {
+        return m;
+    }
+}
+
+// fp64 fast check node. xin: the app values gathered for the row's edges
+// (padding edges read +inf); pv: in = c2v sent last iteration, out = the new
+// c2v. Returns false when the premise may fail for the next iteration (or
+// failed for this one's division).
+template <int DC, int VAR, bool FDIV>
+__device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DC], Pack<double, 1> (&pv)[DC], double alpha,
+                                          double rcp, double delta)
+{
+    constexpr uint32_t SIGN = 0x80000000u;
+    double x[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) x[k] = xin[k].v[0] - pv[k].v[0];   // v2c (:469)
+    double mn1, mn2;
+    two_min<0, DC, DC>(x, mn1, mn2);
+    uint32_t par = 0;
+#pragma unroll
+    for (int k = 0; k + 1 < DC; k += 2) par = __builtin_amdgcn_bitop3_b32(par, hi32(x[k]), hi32(x[k + 1]), 0x96);
+    if (DC & 1) par ^= hi32(x[DC - 1]);
+    const double M1 = norm64<VAR, FDIV>(mn1, alpha, rcp, delta), M2 = norm64<VAR, FDIV>(mn2, alpha, rcp, delta);
+    bool ok = M2 < kFast64Max;   // also false for NaN: M1 <= M2 covers the row
+    if constexpr (VAR == V_NMS && FDIV)
+        ok &= !(mn1 > 0.0 && mn1 < kFast64Tiny) & !(mn2 > 0.0 && mn2 < kFast64Tiny);
+    uint32_t mk1 = SIGN, mk2 = SIGN;
+    if constexpr (VAR == V_OMS) {   // a zeroed message is +0, and sgn(-0.0) = +1 (:511-513)
+        mk1 = (M1 > 0.0 && mn1 != 0.0) ? SIGN : 0u;
+        mk2 = (M2 > 0.0 && mn2 != 0.0) ? SIGN : 0u;
+    }
+    const uint32_t s1 = hi32(M1) ^ (par & mk1), s2 = hi32(M2) ^ (par & mk2);
+    const uint32_t l1 = lo32(M1), l2 = lo32(M2);
+    bool eq[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) eq[k] = __builtin_fabs(x[k]) == mn1;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        const uint32_t h = eq[k] ? s2 : s1, l = eq[k] ? l2 : l1;
+        const uint32_t m = (VAR == V_OMS) ? (eq[k] ? mk2 : mk1) : SIGN;
+        pv[k].v[0] = mkd(l, __builtin_amdgcn_bitop3_b32(h, hi32(x[k]), m, 0x78));   // h ^ (v2c_k & m)
+    }
+    return ok;
+}
+
+template <int RPT> struct FastShape;
+template <> struct FastShape<1> { static constexpr int threads = 1024, waves_per_eu = 4; };
+template <> struct FastShape<2> { static constexpr int threads = 512, waves_per_eu = 4; };
+
+template <typename F, int SRC, int C, int DC, int CPT, int RPT, int VAR, bool FDIV>
+__global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_eu) void k_rows_fast(
+    DecodeArgs a, DevGraph g, RowSched rs, unsigned *redo)
+{
+    static_assert(sizeof(F) == 8 && C == 1, "fp64 fast kernel");
+    using P = Pack<F, C>;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int N = g.N, EA = rs.e_pad + 64;
+    P *app = reinterpret_cast<P *>(smem);          // [N + 2]: bit N is the +INF sentinel of padding edges
+    P *c2v = app + (N + 2);                        // [EA] bit-slot-major; last 64: per-lane dummies
+    int *red = reinterpret_cast<int *>(c2v + EA);  // [31]: premise flag of the current group
+
+    int deg[RPT];
+    uint32_t colw[RPT][DC / 2], posw[RPT][DC / 2];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+        const int j = tid + r * nt;
+        deg[r] = rs.cn_deg[j];
+#pragma unroll
+        for (int q = 0; q < DC / 8; ++q) {
+            const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)j * DC)[q];
+            const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)j * DC)[q];
+            colw[r][4 * q + 0] = xc.x; colw[r][4 * q + 1] = xc.y; colw[r][4 * q + 2] = xc.z; colw[r][4 * q + 3] = xc.w;
+            posw[r][4 * q + 0] = xp.x; posw[r][4 * q + 1] = xp.y; posw[r][4 * q + 2] = xp.z; posw[r][4 * q + 3] = xp.w;
+        }
+    }
+    const int lane = tid & 63;
+    int vgb[CPT], vgd[CPT];
+    uint32_t vdst2[(CPT + 1) / 2] = {};
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = rs.vn_col[tid * CPT + i];
+        vdst2[i / 2] |= (uint32_t)(c == 0xffff ? N + 1 : c) << (16 * (i & 1));
+        const uint32_t info = rs.vn_info[tid * CPT + i];
+        vgb[i] = __builtin_amdgcn_readfirstlane((int)(info & 0xffffu) - lane);
+        vgd[i] = __builtin_amdgcn_readfirstlane((int)(info >> 24));
+    }
+    auto vdst = [&](int i) -> int { return (int)((vdst2[i / 2] >> (16 * (i & 1))) & 0xffffu); };
+    if (tid == 0) {
+        P inf;
+#pragma unroll
+        for (int c = 0; c < C; ++c) inf.v[c] = dinf<F>();
+        app[N] = inf;
+    }
+    if ((tid >> 6) >= (nt >> 7)) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH item 4
+    const F alpha = (F)a.alpha, delta = (F)a.delta, rcp = (F)(1.0 / a.alpha);
+    const int ngrp = (a.batch + C - 1) / C;
+    __shared__ unsigned long long acc[6];   // the block's totals (thread 0), added to a.counts once at the end
+    if (tid == 0)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) acc[q] = 0;
+    for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
+        // ---- channel (:214-238), staged through the c2v area ----
+        if (tid == 0) red[31] = 0;
+        int unc[C];
+        const int8_t *cvec[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            unc[c] = 0;
+            cvec[c] = nullptr;
+            const int b = grp * C + c;
+            if (b >= a.batch) continue;
+            const uint64_t cw = a.first_cw + (uint64_t)b;
+            if (SRC == SRC_GIVEN) {
+                if (a.c) cvec[c] = a.c + (size_t)b * N;
+                const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
+                for (int v = tid; v < N; v += nt) {
+                    const F q = front_end<F>(y[v], a);
+                    c2v[v].v[c] = q;
+                    const int cv = cvec[c] ? cvec[c][v] : 1;
+                    unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
+                }
+            } else {
+                if (a.cw_table) cvec[c] = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+                const F sigma = (F)a.sigma;
+                const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+                for (int g4 = tid; g4 * 4 < N; g4 += nt) {
+                    uint32_t u[4];
+                    philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                    F n[4];
+                    box_muller(u[0], u[1], n[0], n[1]);
+                    box_muller(u[2], u[3], n[2], n[3]);
+#pragma unroll
+                    for (int q4 = 0; q4 < 4; ++q4) {
+                        const int v = g4 * 4 + q4;
+                        if (v < N) {
+                            const int cv = cvec[c] ? cvec[c][v] : 1;
+                            const F yv = (F)cv * (F(1) + sigma * n[q4]);
+                            if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
+                            const F q = front_end<F>(yv, a);
+                            c2v[v].v[c] = q;
+                            unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        P yq[CPT];
+        bool in_ok = true;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const P st = c2v[vdst(i) <= N ? vdst(i) : 0];
+            // yq + 0 maps -0 to +0, so app is never -0 (see the header)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                yq[i].v[c] = st.v[c] + F(0);
+                in_ok &= __builtin_fabs(yq[i].v[c]) < (F)kFast64Max;
+            }
+            app[vdst(i)] = yq[i];   // v2c = yq on the first pass (:364-370)
+        }
+        if (!in_ok) red[31] = 1;
+        __syncthreads();
+        // padding slots of the bit-node layout hold +0 (adding +0 changes no sum)
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int dg = (int)((rs.vn_info[tid * CPT + i] >> 16) & 0xffu);
+            const int base = vgb[i] + lane, gd = vgd[i];
+            P z;
+#pragma unroll
+            for (int c = 0; c < C; ++c) z.v[c] = F(0);
+            for (int k = dg; k < gd; ++k) c2v[base + k * 64] = z;
+        }
+        P prev[RPT][DC];   // c2v sent on each edge last iteration: +0 before the first
+#pragma unroll
+        for (int r = 0; r < RPT; ++r)
+#pragma unroll
+            for (int k = 0; k < DC; ++k)
+#pragma unroll
+                for (int c = 0; c < C; ++c) prev[r][k].v[c] = F(0);
+
+        int flag = red[31];
+        for (int it = 0; it < a.T; ++it) {
+            if (__builtin_amdgcn_readfirstlane(flag) != 0) break;
+            // The packed 16-bit schedule words are opaque per iteration: otherwise
+            // the compiler hoists the 32 unpacked indices out of the loop and
+            // spills them (one scratch load per gather).
+#pragma unroll
+            for (int r = 0; r < RPT; ++r)
+#pragma unroll
+                for (int q = 0; q < DC / 2; ++q) asm volatile("" : "+v"(colw[r][q]), "+v"(posw[r][q]));
+#pragma unroll
+            for (int q = 0; q < (CPT + 1) / 2; ++q) asm volatile("" : "+v"(vdst2[q]));
+            // ---- check nodes (with LDPC_FAST_PREFETCH, row r+1's gathers are issued
+            // before row r is computed) ----
+            P xin[LDPC_FAST_PREFETCH ? 2 : 1][DC];
+#pragma unroll
+            for (int k = 0; k < DC; ++k) xin[0][k] = app[u16_at<DC>(colw[0], k)];
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) {
+                constexpr int NB = LDPC_FAST_PREFETCH ? 2 : 1;
+                if (LDPC_FAST_PREFETCH && r + 1 < RPT) {
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) xin[(r + 1) % NB][k] = app[u16_at<DC>(colw[r + 1 < RPT ? r + 1 : r], k)];
+                }
+                if (!LDPC_FAST_PREFETCH && r > 0) {
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) xin[0][k] = app[u16_at<DC>(colw[r], k)];
+                }
+                const bool ok = cn_fast64<DC, VAR, FDIV>(xin[r % NB], prev[r], alpha, rcp, delta);
+                if (!ok && deg[r] > 0) red[31] = 1;   // rows past M (degree 0) only write dummy slots
+#pragma unroll
+                for (int k = 0; k < DC; ++k) c2v[u16_at<DC>(posw[r], k)] = prev[r][k];
+                if (RPT > 1) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
+            }
+            __syncthreads();
+            flag = red[31];   // in flight during the bit phase
+            // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
+            {
+                P sum[CPT];
+#pragma unroll
+                for (int i = 0; i < CPT; ++i) sum[i] = yq[i];
+                int k = 0;
+                vn_phases<F, C, CPT, CPT>(c2v + lane, vgb, vgd, k, sum);
+#pragma unroll
+                for (int i = 0; i < CPT; ++i) app[vdst(i)] = sum[i];
+            }
+            __syncthreads();
+        }
+        // Any premise failure in this group (flag set after the last barrier
+        // at the latest): decode it again on the exact path.
+        if (__builtin_amdgcn_readfirstlane(red[31]) != 0) {
+            if (tid == 0) {
+                const int nb = (grp * C + C <= a.batch) ? C : a.batch - grp * C;
+                const unsigned at = atomicAdd(&redo[0], (unsigned)nb);
+                for (int c = 0; c < nb; ++c) redo[1 + at + c] = (unsigned)(grp * C + c);
+            }
+            __syncthreads();
+            continue;
+        }
+
+        // ---- decisions, error weight (:270, :382-393), syndrome, accounting ----
+        int sums[3 * C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int b = grp * C + c;
+            int w = 0, synd = 0;
+            if (b < a.batch) {
+#pragma unroll
+                for (int i = 0; i < CPT; ++i) {
+                    const int v = vdst(i);
+                    if (v < N) {
+                        const int d = app[v].v[c] > F(0) ? 1 : -1;   // :471-474
+                        const int cv = cvec[c] ? cvec[c][v] : 1;
+                        w += (d != cv);
+                        if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < RPT; ++r) {   // padding edges read the +inf sentinel: parity 0
+                    int par = 0;
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) par ^= (app[u16_at<DC>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
+                    synd |= par;
+                }
+            }
+            sums[3 * c] = w;
+            sums[3 * c + 1] = unc[c];
+            sums[3 * c + 2] = synd;
+        }
+        block_sum_n<3 * C>(sums, red + 32);
+        if (tid == 0) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int b = grp * C + c;
+                if (b >= a.batch) continue;
+                const int w = sums[3 * c], uc = sums[3 * c + 1], sf = sums[3 * c + 2] > 0;
+                acc[0] += (unsigned long long)w;
+                acc[1] += (unsigned long long)(w > 0);
+                acc[2] += (unsigned long long)uc;
+                acc[3] += 1ull;
+                acc[5] += (unsigned long long)sf;
+                if (w > 0 && a.hist) atomicAdd(&a.hist[w - 1], 1ull);
+                if (a.frame_res) a.frame_res[b] = make_int4(w, uc, sf, 0);
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0 && acc[3] > 0) {
+        acc[4] = acc[3] * (unsigned long long)a.T;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) atomicAdd(&a.counts[q], acc[q]);
+    }
+}
+
+// alpha = P * 2^E with odd P < 2^20, in the range where 1/alpha is normal:
+// Markstein's correction is then exact (header).
+bool markstein_exact_alpha(double alpha)
+{
+    if (!(alpha > 0x1p-900) || !(alpha < 0x1p900)) return false;
+    unsigned long long b;
+    __builtin_memcpy(&b, &alpha, 8);
+    const unsigned long long sig = (b & ((1ull << 52) - 1)) | (1ull << 52);   // 53-bit significand
+    const int tz = __builtin_ctzll(sig);
+    return (sig >> tz) < (1ull << 20);
+}
+
+template <int VAR, bool FDIV, int SRC, int DC, int CPT, int RPT>
+static hipError_t launch_fast_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, int lds, unsigned *redo,
+                                hipStream_t s, int num_cus)
+{
+    auto fn = k_rows_fast<double, SRC, 1, DC, CPT, RPT, VAR, FDIV>;
+    hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    int per_cu = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, rs.threads, lds);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    int grid = per_cu * num_cus;
+    if (grid > a.batch) grid = a.batch;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(rs.threads), lds, s, a, g, rs, redo);
+    return hipGetLastError();
+}
+
+template <int VAR, bool FDIV, int SRC>
+static hipError_t launch_fast_shape(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, int lds, unsigned *redo,
+                                    hipStream_t s, int num_cus)
+{
+#define LDPC_FAST_CASE(DCV, CPTV, RPTV) \
+    if (rs.dc == DCV && rs.cpt == CPTV && rs.rpt == RPTV) return launch_fast_t<VAR, FDIV, SRC, DCV, CPTV, RPTV>(g, rs, a, lds, redo, s, num_cus);
+    LDPC_FAST_CASE(8, 4, 2)
+    LDPC_FAST_CASE(8, 2, 1)
+    LDPC_FAST_CASE(8, 4, 1)
+    LDPC_FAST_CASE(16, 4, 2)
+    LDPC_FAST_CASE(16, 2, 1)
+    LDPC_FAST_CASE(16, 4, 1)
+#undef LDPC_FAST_CASE
+    return hipErrorInvalidValue;
+}
+
+bool rows_fast_supported(const RowSched &rs, bool f64)
+{
+    if (!f64 || rs.threads <= 0) return false;
+    if (rs.dc != 8 && rs.dc != 16) return false;
+    return (rs.rpt == 2 && rs.cpt == 4) || (rs.rpt == 1 && (rs.cpt == 2 || rs.cpt == 4));
+}
+
+hipError_t launch_rows_fast(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, int lds_bytes,
+                            unsigned *redo, hipStream_t s, int num_cus)
+{
+    const bool fdiv = a.variant == V_NMS && markstein_exact_alpha(a.alpha);
+    const bool given = a.src == SRC_GIVEN;
+#define LDPC_FAST_SRC(VARV, FD)                                                                         \
+    return given ? launch_fast_shape<VARV, FD, SRC_GIVEN>(g, rs, a, lds_bytes, redo, s, num_cus)        \
+                 : launch_fast_shape<VARV, FD, SRC_PHILOX>(g, rs, a, lds_bytes, redo, s, num_cus);
+    if (a.variant == V_MS) { LDPC_FAST_SRC(V_MS, false) }
+    if (a.variant == V_OMS) { LDPC_FAST_SRC(V_OMS, false) }
+    if (fdiv) { LDPC_FAST_SRC(V_NMS, true) }
+    LDPC_FAST_SRC(V_NMS, false)
+#undef LDPC_FAST_SRC
+}
+
+}  // namespace ldpc

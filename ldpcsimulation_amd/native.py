@@ -22,7 +22,7 @@ LDPC_OK = 0
 MS, NMS, OMS, BP = 0, 1, 2, 3
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
@@ -171,6 +171,7 @@ def lib():
                            i32),
         "ldpc_ctx_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i32),
         "ldpc_ctx_kernel_info": ([vp, C.POINTER(_Cfg), C.c_char_p, i32, C.POINTER(i32), C.POINTER(i32)], i32),
+        "ldpc_ctx_redo_count": ([vp, C.POINTER(C.c_int64)], i32),
         "ldpc_gdbf_decode_batch": ([vp, vp, vp, i32, C.POINTER(_GdbfCfg), vp, vp, vp, C.POINTER(Counts)], i32),
         "ldpc_gdbf_sim_launch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp], i32),
         "ldpc_gdbf_sim_batch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp, C.POINTER(Counts)],
@@ -208,7 +209,7 @@ EXPORTED = ["ldpc_abi_version", "ldpc_last_error", "ldpc_graph_create", "ldpc_gr
             "ldpc_graph_info", "ldpc_graph_destroy", "ldpc_graph_layers", "ldpc_device_count", "ldpc_ctx_create",
             "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
             "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",
-            "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info",
+            "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info", "ldpc_ctx_redo_count",
             "ldpc_gdbf_decode_batch", "ldpc_gdbf_sim_launch", "ldpc_gdbf_sim_batch", "ldpc_gdbf_kernel_info",
             "ldpc_nb_graph_create", "ldpc_nb_graph_load_alist", "ldpc_nb_graph_info", "ldpc_nb_graph_destroy",
             "ldpc_nb_ctx_create", "ldpc_nb_ctx_set_stream", "ldpc_nb_ctx_destroy", "ldpc_nb_ctx_read_counts",
@@ -318,11 +319,23 @@ class Context:
             if y.dtype != want:
                 raise TypeError(f"y must be {np.dtype(want)} for this precision, got {y.dtype}")
             y = np.ascontiguousarray(y)
-            batch = y.size // N
-        else:
-            batch = y.numel() // N
-        if c is not None and isinstance(c, np.ndarray):
-            c = np.ascontiguousarray(c, dtype=np.int8)
+            size = y.size
+        else:   # torch tensor: the kernel reads batch*N elements of the precision's width
+            want = "torch.float64" if cfg.precision == F64 else "torch.float32"
+            if str(y.dtype) != want:
+                raise TypeError(f"y must be {want} for this precision, got {y.dtype}")
+            size = y.numel()
+        if size % N:
+            raise ValueError(f"y has {size} elements, not a multiple of N={N}")
+        batch = size // N
+        if c is not None:
+            if isinstance(c, np.ndarray):
+                c = np.ascontiguousarray(c, dtype=np.int8)
+            elif str(c.dtype) != "torch.int8":
+                raise TypeError(f"c must be torch.int8 (bipolar +1/-1), got {c.dtype}")
+            csize = c.size if isinstance(c, np.ndarray) else c.numel()
+            if csize != batch * N:
+                raise ValueError(f"c has {csize} elements, y {batch * N}")
         d = np.empty((batch, N), dtype=np.int8) if want_decisions else None
         fr = np.empty(batch, dtype=FRAME_DTYPE) if want_frames else None
         cnt = Counts()
@@ -376,6 +389,12 @@ class Context:
         ms = C.c_float()
         _check(lib().ldpc_ctx_last_kernel_ms(self._h, C.byref(ms)))
         return float(ms.value)
+
+    def redo_count(self) -> int:
+        """Codewords of the last launch the fast fp64 row kernel re-decoded on the exact path."""
+        n = C.c_int64()
+        _check(lib().ldpc_ctx_redo_count(self._h, C.byref(n)))
+        return int(n.value)
 
     def kernel_info(self, cfg: DecoderConfig) -> dict:
         name = C.create_string_buffer(32)

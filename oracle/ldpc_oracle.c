@@ -390,3 +390,54 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
     }
     out[0] = x0; out[1] = x1; out[2] = x2; out[3] = x3;
 }
+
+/* ---------------------------------------------------------------------------
+ * Test helper, not a restatement of the reference: the fp64 fast kernel
+ * (ldpcsimulation_amd/csrc/rows_fast.hip) divides the check-node minima by
+ * alpha as q = x*r, q = fma(fma(-q, alpha, x), r, q) with r = RN(1/alpha),
+ * claimed equal to IEEE x/alpha (the reference's `/= alpha`,
+ * decodeMinSum.cpp:494-499) for alpha = P*2^E, odd P < 2^20, and
+ * 2^-960 <= x < 2^1000. Counts the x of a sample for which that fails: n
+ * splitmix64 draws (uniform significand, exponent uniform in [-960, 999]),
+ * plus for every exponent in that range the significands 1, 2 - ulp and the
+ * multiples k*alpha' (alpha' = alpha's significand) nearest to binade points.
+ * ------------------------------------------------------------------------- */
+static uint64_t splitmix64(uint64_t *s)
+{
+    uint64_t z = (*s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static int markstein_bad(double x, double alpha, double r)
+{
+    const double q = x * r;
+    const double m = fma(fma(-q, alpha, x), r, q);
+    const double d = x / alpha;
+    return memcmp(&m, &d, sizeof m) != 0;
+}
+
+long orc_markstein_mismatch(double alpha, long n, uint64_t seed)
+{
+    const double r = 1.0 / alpha;
+    long bad = 0;
+    uint64_t s = seed;
+    for (long i = 0; i < n; ++i) {
+        const uint64_t u = splitmix64(&s);
+        const int e = (int)(splitmix64(&s) % 1960u) - 960;
+        const double x = ldexp(1.0 + (double)(u >> 12) * 0x1p-52, e);
+        bad += markstein_bad(x, alpha, r);
+    }
+    int ea;
+    const double am = frexp(alpha, &ea) * 2.0;   /* alpha's significand in [1, 2) */
+    for (int e = -960; e < 1000; ++e) {
+        const double edge[2] = {1.0, 2.0 - 0x1p-52};
+        for (int k = 0; k < 2; ++k) bad += markstein_bad(ldexp(edge[k], e), alpha, r);
+        for (int k = 1; k <= 64; ++k) {   /* x near k * alpha': quotients near small integers */
+            double x = ldexp(am * k, e), lo = nextafter(x, 0.0), hi = nextafter(x, INFINITY);
+            bad += markstein_bad(x, alpha, r) + markstein_bad(lo, alpha, r) + markstein_bad(hi, alpha, r);
+        }
+    }
+    return bad;
+}

@@ -159,6 +159,8 @@ int  orc_ems_decode(int N, int M, int q, const int *row_ptr, const int *row_col,
 
 /* Philox4x32-10 (Random123 reference constants). */
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* test helper: x in a sample where x*r + one fma correction != IEEE x/alpha (fp64) */
+long orc_markstein_mismatch(double alpha, long n, uint64_t seed);
 
 #ifdef __cplusplus
 }

@@ -82,6 +82,8 @@ def lib():
             getattr(L, name).argtypes = [C.POINTER(_Alist), C.c_void_p, C.c_int,
                                          C.POINTER(_Cfg), C.c_void_p, C.c_void_p]
         L.orc_philox4x32_10.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_markstein_mismatch.argtypes = [C.c_double, C.c_long, C.c_uint64]
+        L.orc_markstein_mismatch.restype = C.c_long
         L.orc_gdbf_front.argtypes = [C.c_double, C.POINTER(_GdbfCfg), C.POINTER(C.c_int)]
         L.orc_gdbf_front.restype = C.c_double
         L.orc_gdbf_front_f32.argtypes = [C.c_float, C.POINTER(_GdbfCfg), C.POINTER(C.c_int)]
@@ -201,8 +203,10 @@ class Alist:
                                  C.byref(st))
         return n, {k: getattr(st, k) for k, _ in _Stats._fields_}, fw[:min(n, cap)]
 
-    def decode(self, yq: np.ndarray, T: int, cfg: Cfg) -> np.ndarray:
-        """Decode a [B, N] or [N] batch; dtype float64 or float32 selects precision."""
+    def decode(self, yq: np.ndarray, T: int, cfg: Cfg, workers: int = 1) -> np.ndarray:
+        """Decode a [B, N] or [N] batch; dtype float64 or float32 selects precision.
+        workers > 1 decodes frames on that many threads (the C call releases the GIL;
+        every call allocates its own state)."""
         yq = np.ascontiguousarray(yq)
         single = yq.ndim == 1
         yq2 = yq.reshape(-1, self.N)
@@ -210,8 +214,18 @@ class Alist:
         fn = lib().orc_decode_f64 if yq2.dtype == np.float64 else lib().orc_decode_f32
         assert yq2.dtype in (np.float64, np.float32)
         cc = cfg.c()
-        for b in range(yq2.shape[0]):
-            fn(C.byref(self._a), yq2[b].ctypes.data, T, C.byref(cc), d[b].ctypes.data)
+
+        def run(lo, hi):
+            for b in range(lo, hi):
+                fn(C.byref(self._a), yq2[b].ctypes.data, T, C.byref(cc), d[b].ctypes.data)
+        B = yq2.shape[0]
+        if workers <= 1 or B < 2:
+            run(0, B)
+        else:
+            from concurrent.futures import ThreadPoolExecutor
+            step = (B + workers - 1) // workers
+            with ThreadPoolExecutor(workers) as ex:
+                list(ex.map(lambda lo: run(lo, min(B, lo + step)), range(0, B, step)))
         return d[0] if single else d
 
     def decode_layered(self, yq: np.ndarray, T: int, cfg: Cfg, order=None) -> np.ndarray:
@@ -306,6 +320,11 @@ class Alist:
         lib().orc_decode_f64_snap(C.byref(self._a), yq.ctypes.data, T, C.byref(cfg.c()),
                                   d.ctypes.data, snap_it, c2v.ctypes.data, app.ctypes.data)
         return d, c2v, app
+
+
+def markstein_mismatch(alpha: float, n: int, seed: int = 1) -> int:
+    """Count of sampled x where the fast fp64 NMS division differs from IEEE x/alpha."""
+    return int(lib().orc_markstein_mismatch(alpha, n, seed))
 
 
 def quantize(x: float, ymax: float, qbits: int) -> float:

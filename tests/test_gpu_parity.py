@@ -177,8 +177,12 @@ def test_all_kernels_bit_identical(monkeypatch, code):
         names = {k: c.kernel_info(cfg)["kernel"] for k, c in ctxs.items()}
         assert names["lds"] == "lds" and names["global"] == "global" and names["flood"] == "flood"
         if code != "4000.2000.4.244.alist":
-            assert names["default"] == "rows"
+            # fp64: the fast-path row kernel (rows_fast.hip); fp32: the row kernel
+            assert names["default"] == ("rows_fast" if prec == native.F64 else "rows")
         outs = {k: c.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300) for k, c in ctxs.items()}
+        monkeypatch.setenv("LDPC_ROWS", "old")   # the previous row kernel (exact + fast loops in one)
+        outs["rows_old"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
+        monkeypatch.delenv("LDPC_ROWS", raising=False)
         ref = outs["global"]
         for k, o in outs.items():
             for a, b in zip(o[:3], ref[:3]):
