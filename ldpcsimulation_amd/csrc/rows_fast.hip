@@ -126,25 +126,68 @@ __device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DC], Pack
     if (DC & 1) par ^= hi32(x[DC - 1]);
     const double M1 = norm64<VAR, FDIV>(mn1, alpha, rcp, delta), M2 = norm64<VAR, FDIV>(mn2, alpha, rcp, delta);
     bool ok = M2 < kFast64Max;   // also false for NaN: M1 <= M2 covers the row
-    if constexpr (VAR == V_NMS && FDIV)
-        ok &= !(mn1 > 0.0 && mn1 < kFast64Tiny) & !(mn2 > 0.0 && mn2 < kFast64Tiny);
+    if constexpr (VAR == V_NMS && FDIV) {
+        // minima in (0, 2^-960): the one-FMA division may round wrongly (wave-uniform skip, rare)
+        if (__builtin_amdgcn_ballot_w64(mn1 < kFast64Tiny))
+            ok &= !(mn1 > 0.0 && mn1 < kFast64Tiny) & !(mn2 > 0.0 && mn2 < kFast64Tiny);
+    }
     uint32_t mk1 = SIGN, mk2 = SIGN;
     if constexpr (VAR == V_OMS) {   // a zeroed message is +0, and sgn(-0.0) = +1 (:511-513)
         mk1 = (M1 > 0.0 && mn1 != 0.0) ? SIGN : 0u;
         mk2 = (M2 > 0.0 && mn2 != 0.0) ? SIGN : 0u;
     }
-    const uint32_t s1 = hi32(M1) ^ (par & mk1), s2 = hi32(M2) ^ (par & mk2);
+    uint32_t s1 = hi32(M1) ^ (par & mk1), s2 = hi32(M2) ^ (par & mk2);
+    asm("" : "+v"(s1), "+v"(s2));   // keep the parity out of the per-edge select
     const uint32_t l1 = lo32(M1), l2 = lo32(M2);
-    bool eq[DC];
-#pragma unroll
-    for (int k = 0; k < DC; ++k) eq[k] = __builtin_fabs(x[k]) == mn1;
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        const uint32_t h = eq[k] ? s2 : s1, l = eq[k] ? l2 : l1;
-        const uint32_t m = (VAR == V_OMS) ? (eq[k] ? mk2 : mk1) : SIGN;
+        // |v2c_k| == min1 as one v_cmp_eq_f64 with the abs source modifier, used as the select mask
+        const bool eq = __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_fcmp(__builtin_fabs(x[k]), mn1, 1));
+        const uint32_t h = eq ? s2 : s1, l = eq ? l2 : l1;
+        const uint32_t m = (VAR == V_OMS) ? (eq ? mk2 : mk1) : SIGN;
         pv[k].v[0] = mkd(l, __builtin_amdgcn_bitop3_b32(h, hi32(x[k]), m, 0x78));   // h ^ (v2c_k & m)
     }
     return ok;
+}
+
+// LDS byte address of 16-bit entry k of a packed schedule row: base + 8 * entry,
+// one v_mad_u32_u16 (op_sel picks the high half) instead of extract + shift-add.
+template <int DC>
+__device__ __forceinline__ uint32_t addr8(const uint32_t (&w)[DC / 2], int k, uint32_t base)
+{
+    uint32_t a;
+    if (k & 1)
+        asm("v_mad_u32_u16 %0, %1, 8, %2 op_sel:[1,0,0,0]" : "=v"(a) : "v"(w[k >> 1]), "v"(base));
+    else
+        asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(a) : "v"(w[k >> 1]), "v"(base));
+    return a;
+}
+// LDS accesses by 32-bit LDS address (no generic-pointer arithmetic: the
+// address from addr8 goes straight into the ds_read / ds_write).
+__device__ __forceinline__ uint32_t lds_addr_of(const void *p)
+{
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+template <int B> struct LdsWord;
+template <> struct LdsWord<4> { using T = unsigned int; };
+template <> struct LdsWord<8> { using T = unsigned long long; };
+template <> struct LdsWord<16> { using T = unsigned int __attribute__((ext_vector_type(4))); };
+template <typename P>
+__device__ __forceinline__ P lds_at(uint32_t addr)
+{
+    using U = typename LdsWord<sizeof(P)>::T;
+    const U u = *(const __attribute__((address_space(3))) U *)(uintptr_t)addr;
+    P p;
+    __builtin_memcpy(&p, &u, sizeof(P));
+    return p;
+}
+template <typename P>
+__device__ __forceinline__ void lds_put(uint32_t addr, const P &v)
+{
+    using U = typename LdsWord<sizeof(P)>::T;
+    U u;
+    __builtin_memcpy(&u, &v, sizeof(P));
+    *(__attribute__((address_space(3))) U *)(uintptr_t)addr = u;
 }
 
 template <int RPT> struct FastShape;
@@ -162,7 +205,8 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
     const int N = g.N, EA = rs.e_pad + 64;
     P *app = reinterpret_cast<P *>(smem);          // [N + 2]: bit N is the +INF sentinel of padding edges
     P *c2v = app + (N + 2);                        // [EA] bit-slot-major; last 64: per-lane dummies
-    int *red = reinterpret_cast<int *>(c2v + EA);  // [31]: premise flag of the current group
+    int *red = reinterpret_cast<int *>(c2v + EA);  // [31]: premise flag of the current group; [32, 80): sums; [96, 108): acc
+    const uint32_t app_base = lds_addr_of(app), c2v_base = lds_addr_of(c2v);   // LDS byte addresses
 
     int deg[RPT];
     uint32_t colw[RPT][DC / 2], posw[RPT][DC / 2];
@@ -199,7 +243,9 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
     if ((tid >> 6) >= (nt >> 7)) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH item 4
     const F alpha = (F)a.alpha, delta = (F)a.delta, rcp = (F)(1.0 / a.alpha);
     const int ngrp = (a.batch + C - 1) / C;
-    __shared__ unsigned long long acc[6];   // the block's totals (thread 0), added to a.counts once at the end
+    // the block's totals (thread 0), added to a.counts once at the end; in the
+    // dynamic area (no static LDS: app starts at LDS address 0)
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(red + 96);
     if (tid == 0)
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
@@ -299,22 +345,22 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             // before row r is computed) ----
             P xin[LDPC_FAST_PREFETCH ? 2 : 1][DC];
 #pragma unroll
-            for (int k = 0; k < DC; ++k) xin[0][k] = app[u16_at<DC>(colw[0], k)];
+            for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(addr8<DC>(colw[0], k, app_base));
 #pragma unroll
             for (int r = 0; r < RPT; ++r) {
                 constexpr int NB = LDPC_FAST_PREFETCH ? 2 : 1;
                 if (LDPC_FAST_PREFETCH && r + 1 < RPT) {
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) xin[(r + 1) % NB][k] = app[u16_at<DC>(colw[r + 1 < RPT ? r + 1 : r], k)];
+                    for (int k = 0; k < DC; ++k) xin[(r + 1) % NB][k] = lds_at<P>(addr8<DC>(colw[r + 1 < RPT ? r + 1 : r], k, app_base));
                 }
                 if (!LDPC_FAST_PREFETCH && r > 0) {
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) xin[0][k] = app[u16_at<DC>(colw[r], k)];
+                    for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(addr8<DC>(colw[r], k, app_base));
                 }
                 const bool ok = cn_fast64<DC, VAR, FDIV>(xin[r % NB], prev[r], alpha, rcp, delta);
                 if (!ok && deg[r] > 0) red[31] = 1;   // rows past M (degree 0) only write dummy slots
 #pragma unroll
-                for (int k = 0; k < DC; ++k) c2v[u16_at<DC>(posw[r], k)] = prev[r][k];
+                for (int k = 0; k < DC; ++k) lds_put<P>(addr8<DC>(posw[r], k, c2v_base), prev[r][k]);
                 if (RPT > 1) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
             }
             __syncthreads();
@@ -325,7 +371,10 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) sum[i] = yq[i];
                 int k = 0;
-                vn_phases<F, C, CPT, CPT>(c2v + lane, vgb, vgd, k, sum);
+                // the lane id recomputed here (v_mbcnt), so the lane's c2v pointer is not a
+                // loop-long live value (it was spilled)
+                const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+                vn_phases<F, C, CPT, CPT>(c2v + ln, vgb, vgd, k, sum);
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) app[vdst(i)] = sum[i];
             }
