@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 6
+#define LDPC_ABI_VERSION 7
 
 typedef enum {
     LDPC_OK = 0,
@@ -214,6 +214,14 @@ int  ldpc_ctx_kernel_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, char *name
  * the fast kernel). Diagnostic of the fast/exact split; synchronises the
  * stream. No reference counterpart (the reference has one exact path). */
 int  ldpc_ctx_redo_count(ldpc_ctx *ctx, int64_t *n);
+/* Shape of the row kernel ("rows"/"rows_fast") that decodes cfg, for the
+ * on-chip (LDS) roofline model of bench.py: info[8] = {threads per block,
+ * rows per thread, bit slots per thread, padded row degree, padded edge slots
+ * e_pad, codewords per block, LDS bytes per block, blocks per CU}.
+ * LDPC_ERR_UNSUPPORTED when another kernel decodes cfg. Host-only, no device
+ * call. No reference counterpart (diagnostic of decodeMinSum.cpp:247-263's
+ * replacement). */
+int  ldpc_ctx_row_sched_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, int32_t *info);
 
 /* ---- GDBF / NGDBF bit flipping (BASELINE config 4) --------------------- */
 /* src/decodeGDBF.cpp in its parallel-flip mode (mu = 1): syndrome check

@@ -849,6 +849,26 @@ int ldpc_ctx_last_kernel_ms(ldpc_ctx *c, float *ms)
     return LDPC_OK;
 }
 
+int ldpc_ctx_row_sched_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, int32_t *info)
+{
+    if (!c || !cfg || !info) return set_err(LDPC_ERR_INVALID, "null argument");
+    const bool f64 = cfg->precision == LDPC_F64;
+    int rc = check_cfg(c, cfg);
+    if (rc) return rc;
+    const ldpc::KernelChoice kc = select_kernel(c, f64, cfg->schedule, cfg->variant);
+    if (cfg->variant == LDPC_BP || !c->has_rs || std::strcmp(kc.name, "rows") != 0)
+        return set_err(LDPC_ERR_UNSUPPORTED, "the row kernel does not decode this cfg (kernel %s)", kc.name);
+    info[0] = c->rs.threads;
+    info[1] = c->rs.rpt;
+    info[2] = c->rs.cpt;
+    info[3] = c->rs.dc;
+    info[4] = c->rs.e_pad;
+    info[5] = kc.cw_per_block;
+    info[6] = kc.lds_bytes;
+    info[7] = ldpc::blocks_per_cu(c->dg, f64, kc);
+    return LDPC_OK;
+}
+
 int ldpc_ctx_redo_count(ldpc_ctx *c, int64_t *n)
 {
     if (!c || !n) return set_err(LDPC_ERR_INVALID, "null argument");

@@ -22,7 +22,7 @@ LDPC_OK = 0
 MS, NMS, OMS, BP = 0, 1, 2, 3
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
@@ -172,6 +172,7 @@ def lib():
         "ldpc_ctx_last_kernel_ms": ([vp, C.POINTER(C.c_float)], i32),
         "ldpc_ctx_kernel_info": ([vp, C.POINTER(_Cfg), C.c_char_p, i32, C.POINTER(i32), C.POINTER(i32)], i32),
         "ldpc_ctx_redo_count": ([vp, C.POINTER(C.c_int64)], i32),
+        "ldpc_ctx_row_sched_info": ([vp, C.POINTER(_Cfg), vp], i32),
         "ldpc_gdbf_decode_batch": ([vp, vp, vp, i32, C.POINTER(_GdbfCfg), vp, vp, vp, C.POINTER(Counts)], i32),
         "ldpc_gdbf_sim_launch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp], i32),
         "ldpc_gdbf_sim_batch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp, C.POINTER(Counts)],
@@ -210,6 +211,7 @@ EXPORTED = ["ldpc_abi_version", "ldpc_last_error", "ldpc_graph_create", "ldpc_gr
             "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
             "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",
             "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info", "ldpc_ctx_redo_count",
+            "ldpc_ctx_row_sched_info",
             "ldpc_gdbf_decode_batch", "ldpc_gdbf_sim_launch", "ldpc_gdbf_sim_batch", "ldpc_gdbf_kernel_info",
             "ldpc_nb_graph_create", "ldpc_nb_graph_load_alist", "ldpc_nb_graph_info", "ldpc_nb_graph_destroy",
             "ldpc_nb_ctx_create", "ldpc_nb_ctx_set_stream", "ldpc_nb_ctx_destroy", "ldpc_nb_ctx_read_counts",
@@ -395,6 +397,14 @@ class Context:
         n = C.c_int64()
         _check(lib().ldpc_ctx_redo_count(self._h, C.byref(n)))
         return int(n.value)
+
+    def row_sched_info(self, cfg: DecoderConfig) -> dict:
+        """Shape of the row kernel that decodes cfg (raises LdpcError UNSUPPORTED for other kernels)."""
+        info = np.zeros(8, dtype=np.int32)
+        _check(lib().ldpc_ctx_row_sched_info(self._h, C.byref(cfg._c()), info.ctypes.data))
+        keys = ("threads", "rows_per_thread", "slots_per_thread", "dc", "e_pad", "cw_per_block", "lds_bytes",
+                "blocks_per_cu")
+        return {k: int(v) for k, v in zip(keys, info)}
 
     def kernel_info(self, cfg: DecoderConfig) -> dict:
         name = C.create_string_buffer(32)

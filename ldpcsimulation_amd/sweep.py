@@ -76,6 +76,13 @@ def main(argv=None) -> int:
         torch.cuda.set_device(device)
         dist.init_process_group("nccl", device_id=torch.device("cuda", device))
     seed = a.seed if a.seed is not None else int(time.time())
+    if world > 1 and a.seed is None:
+        # every rank must key its noise with rank 0's seed (ranks may start in different seconds)
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([seed], dtype=torch.int64, device=f"cuda:{device}")
+        dist.broadcast(t, src=0)
+        seed = int(t.item())
     if a.ems:
         return _ems_sweep(a, seed, world, rank, device)
     cfg = native.DecoderConfig(variant=VARIANTS[a.variant], T=a.iterations, alpha=a.alpha, delta=a.delta,

@@ -19,7 +19,7 @@ def test_defaults(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = b.parse()
     assert (a.gpus, a.steps, a.warmup) == (1, 5, 2)
-    assert (a.batch, a.T, a.alpha, a.ebn0, a.precision) == (65536, 50, 1.25, 1.5, "f32")
+    assert (a.batch, a.T, a.alpha, a.ebn0, a.precision) == (65536, 50, 1.25, 1.5, "f64")
 
 
 def test_driver_flags(monkeypatch):
@@ -33,3 +33,52 @@ def test_reference_fer_table_matches_survey():
     b = _bench()
     assert b.REF_FER == {1.0: (40, 96), 1.25: (40, 362), 1.5: (40, 2212), 1.75: (40, 41745)}
     assert b.HBM_PEAK == 8.0e12
+
+
+def test_gpus_mismatch_is_rejected(monkeypatch):
+    """--gpus N under a torchrun of another size exits non-zero before any GPU call."""
+    import pytest
+    b = _bench()
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    with pytest.raises(SystemExit) as e:
+        b.main()
+    assert e.value.code not in (0, None)
+
+
+def test_gpus_without_torchrun_spawns_ranks(monkeypatch):
+    """--gpus N with no WORLD_SIZE starts torchrun with N ranks as a child and exits with its status."""
+    import pytest
+    b = _bench()
+    seen = {}
+
+    def fake_call(cmd):
+        seen["cmd"] = cmd
+        return 0
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(b.subprocess, "call", fake_call)
+    with pytest.raises(SystemExit) as e:
+        b.main()
+    assert e.value.code == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=2" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"]
+
+
+def test_lds_model_of_the_n1944_row_schedule():
+    """The LDS roofline model for the N=1944 schedule: 1024 row slots x 8,
+    e_pad 7232, 512 x 4 bit slots -> 1442 LDS-array cycles per group-iteration."""
+    b = _bench()
+    si = {"threads": 512, "rows_per_thread": 2, "slots_per_thread": 4, "dc": 8, "e_pad": 7232,
+          "cw_per_block": 1, "lds_bytes": 74576, "blocks_per_cu": 2}
+    m = b.lds_model(si, 1944)
+    assert m["by_phase"] == {"check_gather": 256, "check_scatter": 768, "bit_read": 226, "app_write": 192}
+    assert m["cycles_per_group_iter"] == 1442
+
+
+def test_cpu_share_is_capped(monkeypatch):
+    b = _bench()
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert 1 <= b.cpu_share() <= 3

@@ -1,0 +1,82 @@
+"""The sharded SNR-point driver (sim.simulate_point, the replacement of the
+reference's per-SNR process model scripts/minsum_example_PEGReg504x1008.sh:23-27
+and the frame loop decodeMinSum.cpp:189-289) on the real HIP path.
+
+Two gloo ranks, spawned processes with their own ldpc context on device 0 (one
+box has one GPU; the data path has no collective beyond the 48-byte counter
+all-reduce, so sharing the card changes nothing but speed), decode config 2
+(802.11n N=1944, NMS alpha=1.25, T=50, fp64, on-device Philox noise) at
+1.5 dB to the reference's stop rule. Their totals and error-weight
+histogram must equal one rank's, for a different batch size too: the frames
+are keyed by global index, and the exact-stop cut makes the result a
+frame-by-frame run of the same noise."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import code_path
+
+CODE = "80211n_1944_r12.alist"
+EBN0, SEED, T = 1.5, 20261018, 50
+
+
+def _cfg():
+    from ldpcsimulation_amd import native
+    return native.DecoderConfig(variant=native.NMS, alpha=1.25, T=T, precision=native.F64)
+
+
+def _run(ctx, batch):
+    from ldpcsimulation_amd import sim
+    cfg = _cfg()
+
+    def run_batch(first, n):
+        fr, _ = ctx.sim_batch(EBN0, 0.5, cfg, SEED, 0, first, n)
+        return fr
+    return sim.simulate_point(run_batch, ctx.graph.N, T, EBN0, batch, device=0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, batch, path, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ldpcsimulation_amd import native
+        ctx = native.Context(native.Graph.from_alist(path), 0, batch)
+        res = _run(ctx, batch)
+        q.put((rank, res.counts, res.hist.tolist(), res.rounds))
+    except Exception as e:   # report, never hang the parent
+        q.put((rank, repr(e), None, None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_the_hip_path_equal_one_rank(gpu_ctx_factory):
+    import torch.multiprocessing as mp
+    one = _run(gpu_ctx_factory(CODE, 2048), 2048)
+    assert one.counts["frame_err"] >= 40 and one.counts["bit_err"] >= 200
+    other_batch = _run(gpu_ctx_factory(CODE, 768), 768)
+    assert other_batch.counts == one.counts and np.array_equal(other_batch.hist, one.hist)
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 1024, code_path(CODE), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, counts, hist, rounds in out:
+        assert isinstance(counts, dict), counts
+        assert counts == one.counts, (rank, counts, one.counts)
+        assert np.array_equal(np.array(hist), one.hist), rank
