@@ -326,8 +326,8 @@ def main():
         traffic, traffic_src = None, None
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("precision", "f32") == args.precision:
-                traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
+            tj = tj.get(args.precision, {})
+            traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
         except (OSError, ValueError):
             pass
         k_fe, n_fe = int(tot[1]), int(tot[3])

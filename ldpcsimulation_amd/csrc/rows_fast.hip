@@ -57,9 +57,17 @@ namespace ldpc {
 #ifndef LDPC_FAST_PREFETCH
 #define LDPC_FAST_PREFETCH 1
 #endif
+// Timing experiments only (wrong results; `make fastvariant`): LDPC_FAST_EXP =
+// 1 no c2v scatters, 2 no bit phase, 3 no barriers in the iteration loop,
+// 4 check node replaced by a copy, 5 gathers all read one address.
+#ifndef LDPC_FAST_EXP
+#define LDPC_FAST_EXP 0
+#endif
 
 constexpr double kFast64Max = 0x1p1000;    // premise bound on |yq| and |c2v|
 constexpr double kFast64Tiny = 0x1p-960;   // Markstein division: minima >= this (or 0)
+constexpr uint32_t kFast64MaxHi = 0x7e700000u;    // high word of 2^1000 (low word 0)
+constexpr uint32_t kFast64TinyHi = 0x03f00000u;   // high word of 2^-960 (low word 0)
 
 __device__ __forceinline__ uint32_t hi32(double d) { return (uint32_t)((unsigned long long)__double_as_longlong(d) >> 32); }
 __device__ __forceinline__ uint32_t lo32(double d) { return (uint32_t)(unsigned long long)__double_as_longlong(d); }
@@ -125,10 +133,12 @@ __device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DC], Pack
     for (int k = 0; k + 1 < DC; k += 2) par = __builtin_amdgcn_bitop3_b32(par, hi32(x[k]), hi32(x[k + 1]), 0x96);
     if (DC & 1) par ^= hi32(x[DC - 1]);
     const double M1 = norm64<VAR, FDIV>(mn1, alpha, rcp, delta), M2 = norm64<VAR, FDIV>(mn2, alpha, rcp, delta);
-    bool ok = M2 < kFast64Max;   // also false for NaN: M1 <= M2 covers the row
+    // M2 < 2^1000 on the high word (M2 >= +0; 2^1000's low word is 0): one 32-bit compare
+    // instead of an f64 one. Also false for NaN. M1 <= M2 covers the row.
+    bool ok = hi32(M2) < kFast64MaxHi;
     if constexpr (VAR == V_NMS && FDIV) {
         // minima in (0, 2^-960): the one-FMA division may round wrongly (wave-uniform skip, rare)
-        if (__builtin_amdgcn_ballot_w64(mn1 < kFast64Tiny))
+        if (__builtin_amdgcn_ballot_w64(hi32(mn1) < kFast64TinyHi))
             ok &= !(mn1 > 0.0 && mn1 < kFast64Tiny) & !(mn2 > 0.0 && mn2 < kFast64Tiny);
     }
     uint32_t mk1 = SIGN, mk2 = SIGN;
@@ -345,28 +355,37 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             // before row r is computed) ----
             P xin[LDPC_FAST_PREFETCH ? 2 : 1][DC];
 #pragma unroll
-            for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(addr8<DC>(colw[0], k, app_base));
+            for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(LDPC_FAST_EXP == 5 ? app_base + 8 * k : addr8<DC>(colw[0], k, app_base));
 #pragma unroll
             for (int r = 0; r < RPT; ++r) {
                 constexpr int NB = LDPC_FAST_PREFETCH ? 2 : 1;
                 if (LDPC_FAST_PREFETCH && r + 1 < RPT) {
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) xin[(r + 1) % NB][k] = lds_at<P>(addr8<DC>(colw[r + 1 < RPT ? r + 1 : r], k, app_base));
+                    for (int k = 0; k < DC; ++k) xin[(r + 1) % NB][k] = lds_at<P>(LDPC_FAST_EXP == 5 ? app_base + 8 * k : addr8<DC>(colw[r + 1 < RPT ? r + 1 : r], k, app_base));
                 }
                 if (!LDPC_FAST_PREFETCH && r > 0) {
 #pragma unroll
                     for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(addr8<DC>(colw[r], k, app_base));
                 }
-                const bool ok = cn_fast64<DC, VAR, FDIV>(xin[r % NB], prev[r], alpha, rcp, delta);
-                if (!ok && deg[r] > 0) red[31] = 1;   // rows past M (degree 0) only write dummy slots
+                bool ok;
+                if constexpr (LDPC_FAST_EXP == 4) {
+                    ok = true;
 #pragma unroll
-                for (int k = 0; k < DC; ++k) lds_put<P>(addr8<DC>(posw[r], k, c2v_base), prev[r][k]);
+                    for (int k = 0; k < DC; ++k) prev[r][k].v[0] = xin[r % NB][k].v[0] - prev[r][k].v[0];
+                } else {
+                    ok = cn_fast64<DC, VAR, FDIV>(xin[r % NB], prev[r], alpha, rcp, delta);
+                }
+                if (!ok && deg[r] > 0) red[31] = 1;   // rows past M (degree 0) only write dummy slots
+                if constexpr (LDPC_FAST_EXP != 1) {
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) lds_put<P>(addr8<DC>(posw[r], k, c2v_base), prev[r][k]);
+                }
                 if (RPT > 1) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
             }
-            __syncthreads();
+            if constexpr (LDPC_FAST_EXP != 3) __syncthreads();
             flag = red[31];   // in flight during the bit phase
             // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
-            {
+            if constexpr (LDPC_FAST_EXP != 2) {
                 P sum[CPT];
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) sum[i] = yq[i];
@@ -378,7 +397,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) app[vdst(i)] = sum[i];
             }
-            __syncthreads();
+            if constexpr (LDPC_FAST_EXP != 3) __syncthreads();
         }
         // Any premise failure in this group (flag set after the last barrier
         // at the latest): decode it again on the exact path.
