@@ -103,6 +103,37 @@ int set_last_error(int code, const std::string &msg)
 }
 }  // namespace ldpc
 
+// Device copy of a host row schedule (graph.cpp build_row_schedule).
+static hipError_t upload_row_sched(const ldpc::RowSchedule &hs, DevBuf &buf, ldpc::RowSched &rs)
+{
+    auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
+    const size_t b_cc = al(2 * hs.cn_cols.size()), b_cp = al(2 * hs.cn_pos.size()), b_cd = al(hs.cn_deg.size()),
+                 b_vc = al(2 * hs.vn_col.size()), b_vi = al(4 * hs.vn_info.size());
+    hipError_t e = buf.ensure(b_cc + b_cp + b_cd + b_vc + b_vi);
+    if (e != hipSuccess) return e;
+    unsigned char *sb = (unsigned char *)buf.p;
+    const std::pair<const void *, size_t> parts[] = {{hs.cn_cols.data(), 2 * hs.cn_cols.size()},
+                                                     {hs.cn_pos.data(), 2 * hs.cn_pos.size()},
+                                                     {hs.cn_deg.data(), hs.cn_deg.size()},
+                                                     {hs.vn_col.data(), 2 * hs.vn_col.size()},
+                                                     {hs.vn_info.data(), 4 * hs.vn_info.size()}};
+    const size_t offs[] = {0, b_cc, b_cc + b_cp, b_cc + b_cp + b_cd, b_cc + b_cp + b_cd + b_vc};
+    for (int i = 0; i < 5; ++i)
+        if (parts[i].second && (e = hipMemcpy(sb + offs[i], parts[i].first, parts[i].second, hipMemcpyHostToDevice)) != hipSuccess)
+            return e;
+    rs.threads = hs.threads;
+    rs.cpt = hs.cpt;
+    rs.dc = hs.dc;
+    rs.e_pad = hs.e_pad;
+    rs.rpt = hs.rpt;
+    rs.cn_cols = (const uint16_t *)sb;
+    rs.cn_pos = (const uint16_t *)(sb + offs[1]);
+    rs.cn_deg = (const uint8_t *)(sb + offs[2]);
+    rs.vn_col = (const uint16_t *)(sb + offs[3]);
+    rs.vn_info = (const uint32_t *)(sb + offs[4]);
+    return hipSuccess;
+}
+
 extern "C" {
 
 int ldpc_abi_version(void) { return LDPC_ABI_VERSION; }
@@ -300,26 +331,7 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
         ldpc::RowSchedule hs;
         if (threads <= ldpc::kRowsMaxThreadsForRpt[rpt] && dc && cpt &&
             ldpc::build_row_schedule(*g, threads, cpt, dc, rpt, hs).empty()) {
-            const size_t b_cc = al(2 * hs.cn_cols.size()), b_cp = al(2 * hs.cn_pos.size()), b_cd = al(hs.cn_deg.size()),
-                         b_vc = al(2 * hs.vn_col.size()), b_vi = al(4 * hs.vn_info.size());
-            CTX_TRY(c->sched.ensure(b_cc + b_cp + b_cd + b_vc + b_vi));
-            unsigned char *sb = (unsigned char *)c->sched.p;
-            CTX_TRY(hipMemcpy(sb, hs.cn_cols.data(), 2 * hs.cn_cols.size(), hipMemcpyHostToDevice));
-            CTX_TRY(hipMemcpy(sb + b_cc, hs.cn_pos.data(), 2 * hs.cn_pos.size(), hipMemcpyHostToDevice));
-            CTX_TRY(hipMemcpy(sb + b_cc + b_cp, hs.cn_deg.data(), hs.cn_deg.size(), hipMemcpyHostToDevice));
-            CTX_TRY(hipMemcpy(sb + b_cc + b_cp + b_cd, hs.vn_col.data(), 2 * hs.vn_col.size(), hipMemcpyHostToDevice));
-            CTX_TRY(hipMemcpy(sb + b_cc + b_cp + b_cd + b_vc, hs.vn_info.data(), 4 * hs.vn_info.size(),
-                              hipMemcpyHostToDevice));
-            c->rs.threads = hs.threads;
-            c->rs.cpt = hs.cpt;
-            c->rs.dc = hs.dc;
-            c->rs.e_pad = hs.e_pad;
-            c->rs.rpt = hs.rpt;
-            c->rs.cn_cols = (const uint16_t *)sb;
-            c->rs.cn_pos = (const uint16_t *)(sb + b_cc);
-            c->rs.cn_deg = (const uint8_t *)(sb + b_cc + b_cp);
-            c->rs.vn_col = (const uint16_t *)(sb + b_cc + b_cp + b_cd);
-            c->rs.vn_info = (const uint32_t *)(sb + b_cc + b_cp + b_cd + b_vc);
+            CTX_TRY(upload_row_sched(hs, c->sched, c->rs));
             c->has_rs = true;
         }
     }
@@ -562,7 +574,8 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
     c->last_fast = fast;
     if (fast) {
         HIP_TRY(hipMemsetAsync(c->redo.p, 0, sizeof(unsigned), c->stream));
-        HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, kc.lds_bytes, (unsigned *)c->redo.p, c->stream, c->num_cus));
+        HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, kc.lds_bytes, (unsigned *)c->redo.p, c->stream,
+                                       c->num_cus));
         HIP_TRY(ldpc::launch_redo(c->dg, a, f64, (const unsigned *)c->redo.p, c->stream, c->num_cus));
     } else if (layered)
         HIP_TRY(ldpc::launch_layered(c->dg, a, f64, kc, c->fs, c->ls, c->gscratch.p, gblocks, c->stream));

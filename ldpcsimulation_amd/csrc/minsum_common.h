@@ -95,11 +95,54 @@ __device__ __forceinline__ void padd<float, 2>(Pack<float, 2> &s, const Pack<flo
 // lane, base_i wave-uniform), in edge order per slot, U edges of every slot in
 // flight per step. (Steps sized exactly to the remainder were measured slower:
 // the extra unrolled variants cost more in instruction fetch than they save.)
+#ifndef LDPC_VN_U3
+#define LDPC_VN_U3 2
+#endif
+#ifndef LDPC_VN_U1
+#define LDPC_VN_U1 4
+#endif
+#ifndef LDPC_VN_PIPE
+#define LDPC_VN_PIPE 0
+#endif
+template <typename F, int C, int NACT, int U, int CPT>
+__device__ __forceinline__ void vn_load(const Pack<F, C> *c2v, const int (&base)[CPT], int k, Pack<F, C> (&r)[NACT][U])
+{
+#pragma unroll
+    for (int i = 0; i < NACT; ++i)
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[i][u] = c2v[base[i] + (k + u) * 64];
+}
+template <typename F, int C, int NACT, int U, int CPT>
+__device__ __forceinline__ void vn_add(const Pack<F, C> (&r)[NACT][U], Pack<F, C> (&sum)[CPT])
+{
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int i = 0; i < NACT; ++i) padd(sum[i], r[i][u]);
+}
 template <typename F, int C, int NACT, int CPT>
 __device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base)[CPT], int &k, int kend,
                                          Pack<F, C> (&sum)[CPT])
 {
-    constexpr int U = NACT >= 3 ? 2 : 4;   // at most 8 packs in flight
+    constexpr int U = NACT >= 3 ? LDPC_VN_U3 : LDPC_VN_U1;   // packs in flight per step: U * NACT
+    if constexpr (LDPC_VN_PIPE) {
+        // two steps in flight: step s+1's reads are issued before step s is added
+        int n = (kend - k) / U;   // wave-uniform
+        if (n > 0) {
+            Pack<F, C> ra[NACT][U], rb[NACT][U];
+            vn_load<F, C, NACT, U, CPT>(c2v, base, k, ra);
+            for (;;) {
+                if (n >= 2) vn_load<F, C, NACT, U, CPT>(c2v, base, k + U, rb);
+                vn_add<F, C, NACT, U, CPT>(ra, sum);
+                k += U;
+                if (--n == 0) break;
+                if (n >= 2) vn_load<F, C, NACT, U, CPT>(c2v, base, k + U, ra);
+                vn_add<F, C, NACT, U, CPT>(rb, sum);
+                k += U;
+                if (--n == 0) break;
+            }
+        }
+    }
     for (; k + U <= kend; k += U) {
         Pack<F, C> r[NACT][U];
 #pragma unroll
