@@ -50,29 +50,29 @@ $(LIB): $(OBJS)
 # -D normalizedMS without quantisation, the BASELINE config-2 variant).
 CLI_SRC = $(CSRC)/cli_minsum.cpp
 CLI_LINK = -L$(LIBDIR) -lldpc_hip -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
-$(BINDIR)/decodeMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeMinSum: $(CLI_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -o $@ $< $(CLI_LINK)
-$(BINDIR)/decodeNMS: $(CLI_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeNMS: $(CLI_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D normalizedMS -o $@ $< $(CLI_LINK)
-$(BINDIR)/decodeNormalizedMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeNormalizedMinSum: $(CLI_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D quantizeSamples -D normalizedMS -o $@ $< $(CLI_LINK)
-$(BINDIR)/decodeOffsetMinSum: $(CLI_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeOffsetMinSum: $(CLI_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D quantizeSamples -D offsetMS -o $@ $< $(CLI_LINK)
 
-$(BINDIR)/decodeBP: $(CLI_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeBP: $(CLI_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D beliefPropagation -o $@ $< $(CLI_LINK)
 
 # GDBF / NGDBF front-ends: the -D switches of C_implementations/Makefile:33-53.
 GDBF_SRC = $(CSRC)/cli_gdbf.cpp
-$(BINDIR)/decodeMNGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeMNGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D addNoise -D thresholdAdaptation -D weightSyndromes -D saturateSamples -o $@ $< $(CLI_LINK)
-$(BINDIR)/decodeSMNGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeSMNGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D addNoise -D thresholdAdaptation -D weightSyndromes -D outputSmoothing -D saturateSamples -o $@ $< $(CLI_LINK)
-$(BINDIR)/decodeATGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeATGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D thresholdAdaptation -o $@ $< $(CLI_LINK)
-$(BINDIR)/decodeSATGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeSATGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D thresholdAdaptation -D outputSmoothing -o $@ $< $(CLI_LINK)
-$(BINDIR)/decodeSMGDBF: $(GDBF_SRC) $(LIB) | $(BINDIR)
+$(BINDIR)/decodeSMGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D outputSmoothing -o $@ $< $(CLI_LINK)
 
 # Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> lib/variants/libldpc_hip_x.so

@@ -389,3 +389,37 @@ def nb_girth_at_least_6(H: NbParityCheck) -> bool:
                     return False
                 seen.add((cs[a], cs[b]))
     return True
+
+
+def read_codeword_file(path: str, N: int) -> np.ndarray:
+    """The codewords (0/1 bits, [rows, N] uint8) a reference run with this codeword
+    file cycles through (decodeMinSum.cpp:193-211): one line per frame, the file
+    rewound when getline() sets eof() -- so a last line without a trailing newline
+    is never used (unless it is the only line). A symbol other than '0'/'1' (short
+    lines included) keeps the previous frame's bit, as the reference leaves c[i]
+    unchanged; the table holds the values of the first pass through the file."""
+    with open(path, "rb") as f:
+        text = f.read().decode("latin-1")
+    lines = text.split("\n")
+    if text.endswith("\n") or len(lines) > 1:
+        lines.pop()
+    if not lines:
+        lines = [""]
+    import numpy as np
+    out = np.zeros((len(lines), N), dtype=np.uint8)
+    cur = np.zeros(N, dtype=np.uint8)
+    bad = 0
+    for r, l in enumerate(lines):
+        for i in range(N):
+            ch = l[i] if i < len(l) else "\0"
+            if ch == "1":
+                cur[i] = 1
+            elif ch == "0":
+                cur[i] = 0
+            else:
+                bad += 1
+        out[r] = cur
+    if bad:
+        import warnings
+        warnings.warn(f"{path}: {bad} invalid symbols (kept the previous frame's bits, as the reference does)")
+    return out

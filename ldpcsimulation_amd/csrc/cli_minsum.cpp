@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "ldpc_hip.h"
+#include "cli_common.h"
 
 using std::cout;
 using std::endl;
@@ -163,10 +164,7 @@ int main(int argc, char *argv[])
     const bool use_cw = (size_t)argc == args.size() + 1;
     if (use_cw) {
         cout << "\nUsing codewords from " << argv[idx] << endl;
-        std::ifstream cf(argv[idx]);
-        std::string s;
-        while (std::getline(cf, s)) cw_lines.push_back(s);
-        if (cw_lines.empty()) cw_lines.push_back(std::string());
+        cw_lines = reference_codeword_lines(argv[idx]);
     } else {
         cout << "\nUsing all-zero sequence.\n";
     }

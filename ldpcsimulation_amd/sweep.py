@@ -105,9 +105,8 @@ def main(argv=None) -> int:
     if min_fe is None:
         min_fe = (5 if g.N > 50000 else 10 if g.N > 10000 else 20) if a.variant == "bp" else 40
     if a.codewords:
-        lines = [l.strip() for l in open(a.codewords) if l.strip()]
-        import numpy as np
-        ctx.set_codewords(np.array([[1 if ch == "1" else 0 for ch in l[:g.N]] for l in lines], dtype=np.uint8))
+        from .codes import read_codeword_file
+        ctx.set_codewords(read_codeword_file(a.codewords, g.N))
     for k, snr in enumerate(a.snr):
         def run_batch(first, n, snr=snr, k=k):
             fr, _ = ctx.sim_batch(snr, a.rate, cfg, seed, k, first, n)

@@ -22,8 +22,15 @@ def run_config(run):
 def cw_lines(run):
     if not run["cwfile"]:
         return None
-    with open(code_path(run["cwfile"])) as f:
-        return [l.rstrip("\n") for l in f if l.strip()]
+    # the lines the reference cycles through (decodeMinSum.cpp:193-200): an unterminated
+    # last line sets eof() as it is read, so the file is rewound instead of using it
+    text = open(code_path(run["cwfile"])).read()
+    lines = text.split("\n")
+    if text.endswith("\n"):
+        lines.pop()
+    elif len(lines) > 1:
+        lines.pop()
+    return [l for l in lines if l.strip()]
 
 
 def final_numbers(final_line):

@@ -82,3 +82,24 @@ def test_cpu_share_is_capped(monkeypatch):
     b = _bench()
     monkeypatch.setenv("OMP_NUM_THREADS", "3")
     assert 1 <= b.cpu_share() <= 3
+
+
+def test_reference_fer_fixture():
+    """tests/golden/reference_fer.json (scripts/ref_fer.py, the reference's own decodeNMS
+    over 10 seeds per point): every seed ends by the stop rule (>= 40 frame errors,
+    >= 200 bit errors), totals add up, and each point agrees with SURVEY §6's single-seed
+    run (|z| < 3). bench.py reads it for its FER comparison."""
+    import json
+    from ldpcsimulation_amd.sim import two_proportion_z
+    b = _bench()
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_fer.json")))
+    assert d["T"] == 50 and d["alpha"] == 1.25 and d["code"] == "80211n_1944_r12.alist"
+    for p in d["points"]:
+        runs = p["runs"]
+        assert len(runs) == 10 and len({r["seed"] for r in runs}) == 10
+        assert all(r["frame_err"] >= 40 and r["bit_err"] >= 200 for r in runs)
+        for k in ("frame_err", "frames", "bit_err"):
+            assert p[k] == sum(r[k] for r in runs)
+        k1, n1 = b.REF_FER[p["ebn0_db"]]
+        assert abs(two_proportion_z(p["frame_err"], p["frames"], k1, n1)) < 3
+    assert b.reference_fer()[1.5] == (400, 27816)

@@ -57,3 +57,22 @@ def test_codeword_fixtures_satisfy_parity(name, data, n):
     assert len(lines) == n
     for l in lines:
         assert len(l) == H.N and sum(H.syndrome(l)) == 0
+
+
+def test_read_codeword_file_follows_the_reference_eof_rule(tmp_path):
+    """decodeMinSum.cpp:193-211: an unterminated last line is never used; invalid
+    symbols keep the previous frame's bit; a terminated file cycles all its lines."""
+    from ldpcsimulation_amd.codes import read_codeword_file
+    import warnings
+    p = tmp_path / "a.enc"
+    p.write_text("0101\n1100\n0011")
+    assert read_codeword_file(str(p), 4).tolist() == [[0, 1, 0, 1], [1, 1, 0, 0]]
+    p.write_text("0101\n1100\n0011\n")
+    assert read_codeword_file(str(p), 4).tolist() == [[0, 1, 0, 1], [1, 1, 0, 0], [0, 0, 1, 1]]
+    p.write_text("0111")
+    assert read_codeword_file(str(p), 4).tolist() == [[0, 1, 1, 1]]
+    p.write_text("1111\n0x0\n")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        got = read_codeword_file(str(p), 4).tolist()
+    assert got == [[1, 1, 1, 1], [0, 1, 0, 1]] and w

@@ -10,6 +10,8 @@ Tiers:
 """
 import math
 
+import os
+
 import numpy as np
 import pytest
 
@@ -235,28 +237,36 @@ def test_syndrome_and_codeword_mode(gpu_ctx_factory):
         ctx.set_codewords(None)
 
 
-def test_fer_matches_reference_statistically(gpu_ctx_factory):
-    """802.11n N=1944 NMS a=1.25 T=50: GPU fp32 Philox FER vs the reference's (REF_SEED=11):
-    two-proportion z-test |z| < 3 at all four SURVEY §8(d) points, 1.0/1.25/1.5/1.75 dB.
-    1.75 dB (reference 40/41745) decodes 8 x 16384 frames so the GPU side holds
-    ~100+ frame errors (collect >= 100 on the GPU)."""
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_fer_matches_reference_statistically(gpu_ctx_factory, prec):
+    """802.11n N=1944 NMS a=1.25 T=50, on-device Philox channel: GPU FER vs the
+    reference's own decodeNMS over 10 seeds per point (tests/golden/reference_fer.json,
+    scripts/ref_fer.py: 400 frame errors per point, decodeMinSum.cpp:189 stop rule),
+    two-proportion z-test |z| < 3 at all four SURVEY §8(d) points. The GPU side
+    decodes 16k-256k frames (>= 250 frame errors per point), so a FER shift of
+    ~20 % would show as |z| > 3. fp64 is the reference's arithmetic; fp32 is the
+    throughput path (its decision gap to fp64 is tests/test_precision_gap.py)."""
+    import json
     native = _native()
     from ldpcsimulation_amd.sim import two_proportion_z
+    with open(os.path.join(os.path.dirname(__file__), "golden", "reference_fer.json")) as f:
+        ref = {p["ebn0_db"]: (p["frame_err"], p["frames"]) for p in json.load(f)["points"]}
     ctx = gpu_ctx_factory("80211n_1944_r12.alist", 16384)
-    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50)
-    ref = {1.0: (40, 96, 1), 1.25: (40, 362, 1), 1.5: (40, 2212, 1), 1.75: (40, 41745, 8)}
-    for ebn0, (k_ref, n_ref, rounds) in ref.items():
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50,
+                               precision=native.F64 if prec == "f64" else native.F32)
+    rounds = {1.0: 1, 1.25: 1, 1.5: 4, 1.75: 16}
+    for ebn0, (k_ref, n_ref) in sorted(ref.items()):
+        assert k_ref >= 400
         ferr = frames = 0
-        for r in range(rounds):
+        for r in range(rounds[ebn0]):
             _, cnt = ctx.sim_batch(ebn0, 0.5, cfg, seed=2026, stream_id=int(ebn0 * 100), first_cw=r * 16384,
                                    batch=16384, want_frames=False)
             ferr += cnt.frame_err
             frames += cnt.frames
-        assert frames == rounds * 16384
+        assert frames == rounds[ebn0] * 16384
         z = two_proportion_z(ferr, frames, k_ref, n_ref)
-        assert abs(z) < 3, (ebn0, ferr, frames, z)
-        if rounds > 1:
-            assert ferr >= 60, (ebn0, ferr, frames)
+        assert abs(z) < 3, (ebn0, ferr, frames, k_ref, n_ref, z)
+        assert ferr >= 200, (ebn0, ferr, frames)
 
 
 @pytest.mark.parametrize("prec", ["f32", "f64"])
