@@ -101,3 +101,14 @@ clean:
 	rm -rf $(LIBDIR) $(BINDIR) oracle/liboracle.so
 
 .PHONY: all oracle ref clean variant fastvariant
+
+# Host-code sanitizer build: graph.cpp (the Tanner-graph compiler)
+# and the CPU oracle under AddressSanitizer + UBSan, driven over code files.
+ASAN_FLAGS = -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all
+build/host_asan: tests/native/host_asan.cpp $(CSRC)/graph.cpp $(CSRC)/graph.h oracle/ldpc_oracle.c oracle/ldpc_oracle.h
+	mkdir -p build
+	gcc $(ASAN_FLAGS) -std=c11 -ffp-contract=off -Ioracle -c -o build/ldpc_oracle_asan.o oracle/ldpc_oracle.c
+	g++ $(ASAN_FLAGS) -std=c++17 -I$(CSRC) -Ioracle -o $@ tests/native/host_asan.cpp $(CSRC)/graph.cpp build/ldpc_oracle_asan.o -lm
+asan: build/host_asan
+	build/host_asan $(ASAN_CODES)
+.PHONY: asan

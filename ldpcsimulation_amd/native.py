@@ -145,6 +145,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"HIP decoder library not built: {LIB_PATH} (run __graft_entry__.build() or `make`)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname
+    # libamdhip64.so.7, DT_NEEDED by file name), and loading this library first
+    # would map /opt/rocm's copy as well -- two runtimes, and torch.cuda then finds
+    # no GPU. Imported first, torch's copy satisfies this library's soname.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, i32, i64, u32, u64, dbl = C.c_void_p, C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
     sig = {

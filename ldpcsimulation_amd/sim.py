@@ -128,27 +128,53 @@ class _Comm:
 def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, ebn0_db: float,
                    batch: int, min_bit_err: int = 200, min_frame_err: int = 40,
                    max_frames: Optional[int] = None, exact_stop: bool = True, device=None,
-                   iters_in_frames: bool = False) -> PointResult:
+                   iters_in_frames: bool = False, launcher=None) -> PointResult:
     """Run one SNR point to the reference's stop rule.
 
     run_batch(first_cw, n) must decode global frames first_cw..first_cw+n-1 on
     this rank and return their per-frame results (FRAME_DTYPE). All ranks of
-    an initialised torch.distributed group must call this together."""
+    an initialised torch.distributed group must call this together.
+
+    launcher (optional, e.g. AsyncLauncher): launch(slot, first_cw, n) starts a
+    round without waiting and collect(slot) returns its frames. Then, once the
+    counts show that at least two more rounds are needed, round k+1 is launched
+    before round k is reduced, so the host-side reduction and the all-reduce
+    overlap the next decode. The results are the same: frames are keyed by
+    global index and a round launched ahead of the stop is discarded."""
     comm = _Comm(device)
     acc = np.zeros(6, dtype=np.int64)
     res = PointResult(ebn0_db, N, T)
     hist_local = np.zeros(N, dtype=np.int64)   # rounds fully counted: this rank's frames
     hist_cut = np.zeros(N, dtype=np.int64)     # the cut round: all ranks' frames (gathered)
     rnd = 0
+    ahead = False          # round rnd already launched (into slot rnd % 2)
+    last = None            # the previous round's all-reduced increments
+
+    def first_of(r):
+        return r * batch * comm.world + comm.rank * batch
+
     while not stop_reached(acc[0], acc[1], min_bit_err, min_frame_err):
         if max_frames is not None and acc[3] >= max_frames:
             break
-        first = rnd * batch * comm.world + comm.rank * batch
-        fr = np.ascontiguousarray(run_batch(first, batch))
+        first = first_of(rnd)
+        if launcher is None:
+            fr = np.ascontiguousarray(run_batch(first, batch))
+        else:
+            if not ahead:
+                launcher.launch(rnd % 2, first, batch)
+            # launch the next round now when it is surely needed: two more rounds like the last one
+            # stay below the stop rule and the frame cap (the decision is the same on every rank)
+            ahead = last is not None and not stop_reached(acc[0] + 2 * last[0], acc[1] + 2 * last[1],
+                                                          min_bit_err, min_frame_err) and \
+                (max_frames is None or acc[3] + 2 * last[3] < max_frames)
+            if ahead:
+                launcher.launch((rnd + 1) % 2, first_of(rnd + 1), batch)
+            fr = np.ascontiguousarray(launcher.collect(rnd % 2))
         raw = fr.view(np.int32).reshape(-1, 4)
         local = np.array([raw[:, 0].sum(), (raw[:, 0] > 0).sum(), raw[:, 1].sum(), len(raw),
                           raw[:, 3].sum() if iters_in_frames else T * len(raw), raw[:, 2].sum()], dtype=np.int64)
         tot = comm.allreduce_sum(local)
+        last = tot
         after = acc + tot
         crossed = stop_reached(after[0], after[1], min_bit_err, min_frame_err)
         limit_hit = max_frames is not None and after[3] > max_frames
@@ -164,6 +190,8 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
             w = raw[:, 0]
             np.add.at(hist_local, w[w > 0] - 1, 1)
         rnd += 1
+    if launcher is not None and ahead:
+        launcher.collect(rnd % 2)   # drain the round launched ahead of the stop (discarded)
     hist = comm.allreduce_sum(hist_local) + hist_cut
     res.counts = dict(zip(COUNT_KEYS, (int(x) for x in acc)))
     res.rounds = rnd
@@ -186,3 +214,31 @@ def two_proportion_z(k1: int, n1: int, k2: int, n2: int) -> float:
     p = (k1 + k2) / (n1 + n2)
     se = math.sqrt(p * (1 - p) * (1 / n1 + 1 / n2))
     return 0.0 if se == 0 else (k1 / n1 - k2 / n2) / se
+
+
+class AsyncLauncher:
+    """Two-slot asynchronous rounds on a native Context (ldpc_sim_launch): each slot
+    has a device buffer of per-frame results, a pinned host copy and an event, all
+    on the context's stream. launch() returns at once; collect() waits for the slot."""
+
+    def __init__(self, ctx, batch: int, run_launch: Callable):
+        import torch
+        self.torch = torch
+        self.stream = torch.cuda.Stream(device=torch.device("cuda", ctx.device))
+        ctx.set_stream(self.stream.cuda_stream)
+        self.run_launch = run_launch       # run_launch(first_cw, n, frames_dev_tensor)
+        self.dev = [torch.empty((batch, 4), dtype=torch.int32, device=f"cuda:{ctx.device}") for _ in range(2)]
+        self.host = [torch.empty((batch, 4), dtype=torch.int32).pin_memory() for _ in range(2)]
+        self.ev = [torch.cuda.Event() for _ in range(2)]
+        self.n = [0, 0]
+
+    def launch(self, slot: int, first: int, n: int):
+        with self.torch.cuda.stream(self.stream):
+            self.run_launch(first, n, self.dev[slot][:n])
+            self.host[slot][:n].copy_(self.dev[slot][:n], non_blocking=True)
+            self.ev[slot].record(self.stream)
+        self.n[slot] = n
+
+    def collect(self, slot: int) -> np.ndarray:
+        self.ev[slot].synchronize()
+        return self.host[slot][: self.n[slot]].numpy().copy().view(FRAME_DTYPE).reshape(-1)

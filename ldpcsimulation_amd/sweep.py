@@ -61,6 +61,8 @@ def parse(argv=None):
     p.add_argument("--codewords", help="codeword file ('0'/'1' lines), as the reference's optional argument")
     p.add_argument("--log", help="append the reference's tab-separated result line per point")
     p.add_argument("--json", action="store_true", help="also print one JSON object per point")
+    p.add_argument("--sync", action="store_true",
+                   help="one blocking round at a time (default: the next round decodes while one is reduced)")
     return p.parse_args(argv)
 
 
@@ -111,9 +113,16 @@ def main(argv=None) -> int:
         def run_batch(first, n, snr=snr, k=k):
             fr, _ = ctx.sim_batch(snr, a.rate, cfg, seed, k, first, n)
             return fr
+
+        launcher = None
+        if not a.sync:
+            # rounds run ahead: round k+1 decodes while round k is reduced (sim.AsyncLauncher)
+            def run_launch(first, n, frames_dev, snr=snr, k=k):
+                ctx.sim_launch(snr, a.rate, cfg, seed, k, first, n, frames_dev)
+            launcher = sim.AsyncLauncher(ctx, a.batch, run_launch)
         t0 = time.perf_counter()
         res = sim.simulate_point(run_batch, g.N, a.iterations, snr, a.batch, a.min_bit_errors,
-                                 min_fe, a.max_frames, device=device)
+                                 min_fe, a.max_frames, device=device, launcher=launcher)
         dt = time.perf_counter() - t0
         if rank == 0:
             line = res.log_line(a.alist, extra)

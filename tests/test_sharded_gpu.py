@@ -37,6 +37,19 @@ def _run(ctx, batch):
     return sim.simulate_point(run_batch, ctx.graph.N, T, EBN0, batch, device=0)
 
 
+def _run_async(ctx, batch):
+    from ldpcsimulation_amd import sim
+    cfg = _cfg()
+
+    def run_launch(first, n, frames_dev):
+        ctx.sim_launch(EBN0, 0.5, cfg, SEED, 0, first, n, frames_dev)
+    launcher = sim.AsyncLauncher(ctx, batch, run_launch)
+    try:
+        return sim.simulate_point(None, ctx.graph.N, T, EBN0, batch, device=0, launcher=launcher)
+    finally:
+        ctx.set_stream(None)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -65,6 +78,10 @@ def test_two_ranks_on_the_hip_path_equal_one_rank(gpu_ctx_factory):
     assert one.counts["frame_err"] >= 40 and one.counts["bit_err"] >= 200
     other_batch = _run(gpu_ctx_factory(CODE, 768), 768)
     assert other_batch.counts == one.counts and np.array_equal(other_batch.hist, one.hist)
+    # rounds launched ahead (sim.AsyncLauncher: round k+1 decodes while round k is reduced)
+    piped = _run_async(gpu_ctx_factory(CODE, 512), 512)
+    assert piped.counts == one.counts and np.array_equal(piped.hist, one.hist)
+    assert piped.rounds >= 4
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -130,3 +130,44 @@ def test_exact_stop_counts_reported_iterations(batch):
     assert res.counts["frames"] == want["frames"] and res.counts["bit_err"] == want["bit_err"]
     assert res.counts["iters"] == int(frames["iters"].sum())
     assert res.avg_iters < T
+
+
+class _FakeLauncher:
+    """Two-slot launcher over the fake frames, recording what was launched."""
+
+    def __init__(self):
+        self.pending = {}
+        self.launched = []
+
+    def launch(self, slot, first, n):
+        assert slot not in self.pending, "slot reused before it was collected"
+        self.pending[slot] = (first, n)
+        self.launched.append(first)
+
+    def collect(self, slot):
+        first, n = self.pending.pop(slot)
+        return fake_frames(first, n)
+
+
+@pytest.mark.parametrize("batch", [7, 64, 1000])
+def test_pipelined_rounds_identical_to_sequential(batch):
+    """simulate_point with a launcher (round k+1 launched before round k is reduced)
+    gives the sequential totals; every launched slot is collected; at most one round
+    beyond the last needed one is launched."""
+    want, hist = sequential()
+    L = _FakeLauncher()
+    res = sim.simulate_point(fake_frames, N, T, 1.5, batch, launcher=L)
+    assert res.counts == want and np.array_equal(res.hist, hist)
+    assert not L.pending
+    assert len(L.launched) <= res.rounds + 1
+    assert L.launched == sorted(set(L.launched))
+    if res.rounds > 4:
+        assert len(L.launched) == res.rounds + 1 or len(L.launched) == res.rounds
+
+
+def test_pipelined_rounds_respect_max_frames():
+    want, _ = sequential(min_bit=10 ** 9, min_frame=10 ** 9, max_frames=777)
+    L = _FakeLauncher()
+    res = sim.simulate_point(fake_frames, N, T, 1.5, 50, min_bit_err=10 ** 9, min_frame_err=10 ** 9,
+                             max_frames=777, launcher=L)
+    assert res.counts == want and not L.pending
