@@ -86,6 +86,9 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-procs", type=int, default=0, help="0 = the box's CPU share (see cpu_share())")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="collective backend for N>1 (gloo + --share-device: rehearse N ranks on one GPU)")
+    p.add_argument("--share-device", action="store_true", help="every rank on device 0 (rehearsal only)")
     return p.parse_args(argv)
 
 
@@ -233,11 +236,17 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.share_device:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
+    coll_dev = "cuda" if args.backend == "nccl" else "cpu"
 
     from ldpcsimulation_amd import codes, native
     alist = codes.ensure_80211n_1944()
@@ -279,8 +288,8 @@ def main():
         kern_ms = [a.elapsed_time(b) for a, b in ev]
         redo = ctx.redo_count()
         cnt = ctx.read_counts(reset=True).as_array()
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        c = torch.from_numpy(np.append(cnt, redo)).cuda()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+        c = torch.from_numpy(np.append(cnt, redo)).to(coll_dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(c)

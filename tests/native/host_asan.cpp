@@ -86,8 +86,8 @@ static void one_code(const char *path)
     orc_stats st{};
     const int64_t fr = orc_minsum_run(&H, 0.5, 1.0, T, &cfg, 3, nullptr, 0, 3, nullptr, 0, &st);
     CHECK(fr == 3 && st.words == 3, "%s: frame loop", path);
-    std::printf("%s: N=%d M=%d E=%d, %d row schedules, flood %s\n", path, g.N, g.M, g.E, rows,
-                ef.empty() ? "ok" : ef.c_str());
+    std::printf("%s: N=%d M=%d E=%d, %d row schedules, flood %s (coalesced slot accesses %.3f, %d groups)\n", path,
+                g.N, g.M, g.E, rows, ef.empty() ? "ok" : ef.c_str(), fs.coalesced, fs.ngroups);
     orc_alist_free(&H);
 }
 
