@@ -14,7 +14,8 @@ CXXFLAGS  = -O2 -std=c++17 -ffp-contract=off -Iinclude -Wall
 LIB       = $(LIBDIR)/libldpc_hip.so
 OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
 CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalizedMinSum $(BINDIR)/decodeOffsetMinSum \
-            $(BINDIR)/decodeMNGDBF $(BINDIR)/decodeSMNGDBF $(BINDIR)/decodeATGDBF $(BINDIR)/decodeSATGDBF $(BINDIR)/decodeSMGDBF $(BINDIR)/decodeBP
+            $(BINDIR)/decodeMNGDBF $(BINDIR)/decodeSMNGDBF $(BINDIR)/decodeATGDBF $(BINDIR)/decodeSATGDBF $(BINDIR)/decodeSMGDBF $(BINDIR)/decodeBP \
+            $(BINDIR)/decodeSGDBF $(BINDIR)/decodeMGDBF $(BINDIR)/decodeStochasticNGDBF
 
 all: $(LIB) $(CLIS) oracle
 
@@ -30,7 +31,7 @@ $(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h $(CSRC)/device_co
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/rows_fast.o: $(CSRC)/rows_fast.hip $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
-$(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
+$(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/bp.o: $(CSRC)/bp.hip $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -74,6 +75,13 @@ $(BINDIR)/decodeSATGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D thresholdAdaptation -D outputSmoothing -o $@ $< $(CLI_LINK)
 $(BINDIR)/decodeSMGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D outputSmoothing -o $@ $< $(CLI_LINK)
+# single-bit-flip schedules and stochastic flipping (Makefile:24-31)
+$(BINDIR)/decodeSGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
+	g++ $(CXXFLAGS) -D sequentialmode -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeMGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
+	g++ $(CXXFLAGS) -D modeswitching -o $@ $< $(CLI_LINK)
+$(BINDIR)/decodeStochasticNGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
+	g++ $(CXXFLAGS) -D quantizeSamples -D quantizeProbabilities -D weightSyndromes -D saturateSamples -o $@ $< $(CLI_LINK)
 
 # Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> lib/variants/libldpc_hip_x.so
 variant:

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 7
+#define LDPC_ABI_VERSION 8
 
 typedef enum {
     LDPC_OK = 0,
@@ -229,15 +229,25 @@ int  ldpc_ctx_row_sched_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, int32_t
  * [+ perturbation] and flip when E < theta (:536-621). The compile-time
  * switches of C_implementations/Makefile:33-53 are runtime flags:
  * decodeMNGDBF = NOISE|ADAPT|WEIGHT|SATURATE, decodeSMNGDBF = the same|SMOOTH,
- * decodeATGDBF = ADAPT, decodeSATGDBF = ADAPT|SMOOTH, decodeSMGDBF = SMOOTH.
- * (modeswitching / sequentialmode / quantizeProbabilities: not supported.) */
+ * decodeATGDBF = ADAPT, decodeSATGDBF = ADAPT|SMOOTH, decodeSMGDBF = SMOOTH,
+ * and (ABI 8, Makefile:24-31) decodeSGDBF = SEQUENTIAL, decodeMGDBF =
+ * MODESWITCH, decodeStochasticNGDBF = QUANTIZE|QPROB|WEIGHT|SATURATE.
+ * ADAPT with SEQUENTIAL/MODESWITCH and NOISE with QPROB are not supported
+ * (no reference target combines them). */
 typedef enum {
     LDPC_GDBF_NOISE = 1,      /* -D addNoise: E += noiseScale*sigma*n per bit and iteration */
     LDPC_GDBF_ADAPT = 2,      /* -D thresholdAdaptation: theta *= lambda when not flipped   */
     LDPC_GDBF_WEIGHT = 4,     /* -D weightSyndromes: syndrome weight alpha (else 1)         */
     LDPC_GDBF_SMOOTH = 8,     /* -D outputSmoothing: majority of the last windowsize d's    */
     LDPC_GDBF_SATURATE = 16,  /* -D saturateSamples: |yq| <= Ymax                           */
-    LDPC_GDBF_QUANTIZE = 32   /* -D quantizeSamples: quantize(yq) with NQ levels            */
+    LDPC_GDBF_QUANTIZE = 32,  /* -D quantizeSamples: quantize(yq) with NQ levels            */
+    LDPC_GDBF_SEQUENTIAL = 64,   /* -D sequentialmode: flip only the first bit of least energy
+                                    per iteration (mu = 0, :573-580, :619-620)              */
+    LDPC_GDBF_MODESWITCH = 128,  /* -D modeswitching: parallel flips until, after Tswitch,
+                                    the objective sum(d*yq)+sum(s) does not grow (:309-345);
+                                    then sequential                                         */
+    LDPC_GDBF_QPROB = 256        /* -D quantizeProbabilities: flip with probability
+                                    normalCDF((theta-E)/qsigma) rounded to 8 levels (:562-597) */
 } ldpc_gdbf_flag;
 
 typedef struct {
@@ -246,19 +256,23 @@ typedef struct {
     int32_t T;            /* num_iterations (maximum; early stop)         */
     int32_t windowsize;   /* outputSmoothing window                       */
     int32_t nq;           /* quantizeSamples NQ                           */
-    int32_t reserved;     /* 0                                            */
+    int32_t tswitch;      /* MODESWITCH: Tswitch (0 in the reference, :51) */
     double  theta;        /* initial flip threshold                       */
     double  lambda;       /* threshold adaptation factor                  */
     double  alpha;        /* syndrome weight (weightSyndromes)            */
     double  noise_scale;  /* perturbation sigma = noise_scale * channel sigma */
     double  ymax;         /* saturation / quantizer range                 */
+    double  qsigma;       /* QPROB, ldpc_gdbf_decode_batch only: the normalCDF sigma
+                           * (noiseSigma = noise_scale * channel sigma, :296); the sim
+                           * entry points compute it from Eb/N0 and R (ABI 8) */
 } ldpc_gdbf_cfg;
 
 /* Decode `batch` frames of given RAW channel samples y[batch][N] (float for
  * F32, double for F64; host or device): front-end (:254-267), then the
  * iterations with the caller's perturbations pert[batch][T][N] (iteration it
- * of frame b adds pert[b][it][i] to E_i; required with LDPC_GDBF_NOISE, else
- * ignored). c, d_out, frames, counts as ldpc_decode_batch; frames[].iters and
+ * of frame b adds pert[b][it][i] to E_i; required with LDPC_GDBF_NOISE; with
+ * LDPC_GDBF_QPROB pert[b][it][i] is instead the uniform draw ranu() of bit i
+ * in iteration it (:588); else ignored). c, d_out, frames, counts as ldpc_decode_batch; frames[].iters and
  * counts->iters report the iterations run. Synchronous. Replaces the frame
  * body of decodeGDBF.cpp main() (:250-399). */
 int  ldpc_gdbf_decode_batch(ldpc_ctx *ctx, const void *y, const void *pert, int batch, const ldpc_gdbf_cfg *cfg,

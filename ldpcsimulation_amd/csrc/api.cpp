@@ -920,7 +920,12 @@ static int gdbf_check_cfg(const ldpc_gdbf_cfg *cfg)
     if (cfg->precision != LDPC_F32 && cfg->precision != LDPC_F64)
         return set_err(LDPC_ERR_INVALID, "bad precision %d", cfg->precision);
     if (cfg->T < 0 || cfg->T > 4094) return set_err(LDPC_ERR_INVALID, "T must be in 0..4094");
-    if (cfg->flags & ~63) return set_err(LDPC_ERR_INVALID, "unknown GDBF flags 0x%x", cfg->flags);
+    if (cfg->flags & ~511) return set_err(LDPC_ERR_INVALID, "unknown GDBF flags 0x%x", cfg->flags);
+    if ((cfg->flags & LDPC_GDBF_ADAPT) && (cfg->flags & (LDPC_GDBF_SEQUENTIAL | LDPC_GDBF_MODESWITCH)))
+        return set_err(LDPC_ERR_UNSUPPORTED, "threshold adaptation with single-bit flips is not supported");
+    if ((cfg->flags & LDPC_GDBF_QPROB) && (cfg->flags & LDPC_GDBF_NOISE))
+        return set_err(LDPC_ERR_UNSUPPORTED, "QPROB with NOISE is not supported");
+    if ((cfg->flags & LDPC_GDBF_MODESWITCH) && cfg->tswitch < 0) return set_err(LDPC_ERR_INVALID, "tswitch < 0");
     if ((cfg->flags & (LDPC_GDBF_SATURATE | LDPC_GDBF_QUANTIZE)) && !(cfg->ymax > 0))
         return set_err(LDPC_ERR_INVALID, "saturate/quantize need ymax > 0");
     if ((cfg->flags & LDPC_GDBF_QUANTIZE) && (cfg->nq < 1 || cfg->nq > 30))
@@ -942,6 +947,8 @@ static void gdbf_fill(ldpc::GdbfArgs &a, ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, 
     a.w = (cfg->flags & LDPC_GDBF_WEIGHT) ? cfg->alpha : 1.0;   // :541-551
     a.ymax = cfg->ymax;
     a.qmax = std::pow(2, (cfg->nq - 1));                       // :490
+    a.tswitch = cfg->tswitch;
+    a.qsigma = cfg->qsigma;
     a.counts = (unsigned long long *)c->counts.p;
     a.hist = (unsigned long long *)c->hist.p;
 }
@@ -987,7 +994,9 @@ int ldpc_gdbf_decode_batch(ldpc_ctx *c, const void *y, const void *pert, int bat
     if (rc) return rc;
     if (batch <= 0 || batch > c->max_batch)
         return set_err(LDPC_ERR_INVALID, "batch %d outside 1..max_batch=%d", batch, c->max_batch);
-    if ((cfg->flags & LDPC_GDBF_NOISE) && !pert) return set_err(LDPC_ERR_INVALID, "NOISE needs pert");
+    if ((cfg->flags & (LDPC_GDBF_NOISE | LDPC_GDBF_QPROB)) && !pert)
+        return set_err(LDPC_ERR_INVALID, "NOISE / QPROB need pert");
+    if ((cfg->flags & LDPC_GDBF_QPROB) && !(cfg->qsigma > 0)) return set_err(LDPC_ERR_INVALID, "QPROB needs qsigma > 0");
     HIP_TRY(hipSetDevice(c->device));
     const bool f64 = cfg->precision == LDPC_F64;
     const int N = c->g->N;
@@ -1002,7 +1011,7 @@ int ldpc_gdbf_decode_batch(ldpc_ctx *c, const void *y, const void *pert, int bat
         HIP_TRY(hipMemcpyAsync(c->y_stage.p, y, nb * fsz, hipMemcpyHostToDevice, c->stream));
         a.y = c->y_stage.p;
     }
-    if (cfg->flags & LDPC_GDBF_NOISE) {
+    if (cfg->flags & (LDPC_GDBF_NOISE | LDPC_GDBF_QPROB)) {
         const size_t pb = nb * (size_t)cfg->T * fsz;
         if (is_device_ptr(pert)) {
             a.pert = pert;
@@ -1064,6 +1073,7 @@ static int gdbf_sim_impl(ldpc_ctx *c, double ebn0_db, double R, const ldpc_gdbf_
     const double N0 = std::pow(10.0, -ebn0_db / 10.0) / R;   // :175-176
     a.sigma = std::sqrt(N0 / 2.0);
     a.noise_sigma = a.sigma * cfg->noise_scale;               // :296
+    a.qsigma = a.noise_sigma;                                  // symNodeUpdates' sigma (:353, :563)
     a.seed = seed;
     a.stream_id = stream_id;
     a.first_cw = first_cw;
@@ -1106,9 +1116,9 @@ int ldpc_gdbf_sim_batch(ldpc_ctx *c, double ebn0_db, double R, const ldpc_gdbf_c
 
 int ldpc_gdbf_kernel_info(ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, char *name, int name_len, int *lds_bytes)
 {
-    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
     int rc = gdbf_check_cfg(cfg);
     if (rc) return rc;
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
     const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, cfg->precision == LDPC_F64);
     if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", ch.name);
     if (lds_bytes) *lds_bytes = ch.lds_bytes;

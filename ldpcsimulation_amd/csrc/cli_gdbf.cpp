@@ -69,6 +69,7 @@ struct GlibcRandom {
         return (int32_t)(v >> 1);
     }
     double ranf() { return (double)next() / (1.0 + (double)0x7fffffff); }   // rand.h:10-11
+    double ranu() { return (1.0 + (double)next()) / (2.0 + (double)0x7fffffff); }   // rand.h:13-14
     double rann()                                                            // rand.h:19-20
     {
         const double ua = ranf();
@@ -108,7 +109,7 @@ void alist_header(const char *path, int &dv, int &dc)
 int main(int argc, char *argv[])
 {
     std::vector<std::string> args = {"alist", "R", "SNR", "T", "theta", "logfilename"};   // :88-113
-#if defined(addNoise)
+#if defined(addNoise) || defined(quantizeProbabilities)
     args.push_back("noiseScale");
 #endif
 #ifdef quantizeSamples
@@ -161,10 +162,21 @@ int main(int argc, char *argv[])
     cfg.theta = theta;
     const std::string logfilename(argv[idx++]);
     cout << " log = \t" << logfilename << endl;
-#if defined(addNoise)
-    cfg.flags |= LDPC_GDBF_NOISE;
+#if defined(addNoise) || defined(quantizeProbabilities)
     cfg.noise_scale = std::atof(argv[idx++]);
     cout << " noiseScale = \t" << cfg.noise_scale << endl;
+#endif
+#ifdef addNoise
+    cfg.flags |= LDPC_GDBF_NOISE;
+#endif
+#ifdef quantizeProbabilities
+    cfg.flags |= LDPC_GDBF_QPROB;   // :562-597
+#endif
+#ifdef sequentialmode
+    cfg.flags |= LDPC_GDBF_SEQUENTIAL;   // :285-289
+#endif
+#ifdef modeswitching
+    cfg.flags |= LDPC_GDBF_MODESWITCH;   // :309-345, Tswitch = 0 (:51)
 #endif
 #ifdef quantizeSamples
     cfg.flags |= LDPC_GDBF_QUANTIZE;
@@ -259,10 +271,11 @@ int main(int argc, char *argv[])
     std::vector<double> y, pert;
     std::vector<float> yf, pf;
     const bool noise = (cfg.flags & LDPC_GDBF_NOISE) != 0;
+    const bool qprob = (cfg.flags & LDPC_GDBF_QPROB) != 0;   // ranu() per bit and iteration (:588)
     const double noiseSigma = sigma * cfg.noise_scale;   // :296
     if (!philox) {
         y.resize(N);
-        if (noise) pert.resize((size_t)N * (T > 0 ? T : 1));
+        if (noise || qprob) pert.resize((size_t)N * (T > 0 ? T : 1));
     }
     long generated = 0;
     bool done = false;
@@ -279,18 +292,25 @@ int main(int argc, char *argv[])
                 GlibcRandom ahead = g;
                 for (size_t k = 0; k < pert.size(); ++k) pert[k] = noiseSigma * ahead.rann();
             }
-            const void *yin = y.data(), *pin = noise ? pert.data() : nullptr;
+            if (qprob) {
+                GlibcRandom ahead = g;
+                for (size_t k = 0; k < pert.size(); ++k) pert[k] = ahead.ranu();
+                cfg.qsigma = noiseSigma;   // symNodeUpdates' sigma (:296, :353)
+            }
+            const void *yin = y.data(), *pin = (noise || qprob) ? pert.data() : nullptr;
             if (cfg.precision == LDPC_F32) {
                 yf.assign(y.begin(), y.end());
                 pf.assign(pert.begin(), pert.end());
                 yin = yf.data();
-                pin = noise ? pf.data() : nullptr;
+                pin = (noise || qprob) ? pf.data() : nullptr;
             }
             if (ldpc_gdbf_decode_batch(ctx, yin, pin, 1, &cfg, use_cw ? c_cur.data() : nullptr, nullptr, res.data(),
                                        nullptr) != LDPC_OK)
                 die("decoding frame");
             if (noise)   // advance by the rows the decoder drew (one per iteration run, :318-333)
                 for (long k = 0; k < (long)N * res[0].iters; ++k) (void)g.rann();
+            if (qprob)
+                for (long k = 0; k < (long)N * res[0].iters; ++k) (void)g.ranu();
         }
         generated += batch;
         for (int f = 0; f < batch; ++f) {

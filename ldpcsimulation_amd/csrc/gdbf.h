@@ -5,13 +5,18 @@
 namespace ldpc {
 
 // The -D switches of src/decodeGDBF.cpp (values = LDPC_GDBF_* of ldpc_hip.h).
-enum { GDBF_NOISE = 1, GDBF_ADAPT = 2, GDBF_WEIGHT = 4, GDBF_SMOOTH = 8, GDBF_SATURATE = 16, GDBF_QUANTIZE = 32 };
+enum {
+    GDBF_NOISE = 1, GDBF_ADAPT = 2, GDBF_WEIGHT = 4, GDBF_SMOOTH = 8, GDBF_SATURATE = 16, GDBF_QUANTIZE = 32,
+    GDBF_SEQUENTIAL = 64, GDBF_MODESWITCH = 128, GDBF_QPROB = 256
+};
 
 struct GdbfArgs {
-    int batch, T, flags, windowsize, src;
+    int batch, T, flags, windowsize, src, tswitch;
     double theta0, lambda, w, noise_sigma, ymax, qmax, sigma;
+    double qsigma;                  // GDBF_QPROB: the normalCDF sigma (noiseSigma)
     const void *y;                  // SRC_GIVEN: raw channel samples [batch][N] (F)
-    const void *pert;               // SRC_GIVEN with GDBF_NOISE: perturbations [batch][T][N] (F)
+    const void *pert;               // SRC_GIVEN with GDBF_NOISE: perturbations [batch][T][N] (F);
+                                    // with GDBF_QPROB: the ranu() draws [batch][T][N] (F)
     const int8_t *c;                // SRC_GIVEN: bipolar codewords [batch][N] or null (+1)
     const int8_t *cw_table;         // SRC_PHILOX: codeword table [cw_rows][N] or null
     int cw_rows;

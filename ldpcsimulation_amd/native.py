@@ -22,7 +22,7 @@ LDPC_OK = 0
 MS, NMS, OMS, BP = 0, 1, 2, 3
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
@@ -55,6 +55,7 @@ class _Cfg(C.Structure):
 
 
 GDBF_NOISE, GDBF_ADAPT, GDBF_WEIGHT, GDBF_SMOOTH, GDBF_SATURATE, GDBF_QUANTIZE = 1, 2, 4, 8, 16, 32
+GDBF_SEQUENTIAL, GDBF_MODESWITCH, GDBF_QPROB = 64, 128, 256
 # the reference's decodeGDBF.cpp Makefile targets (C_implementations/Makefile:33-53)
 GDBF_VARIANTS = {
     "MNGDBF": GDBF_NOISE | GDBF_ADAPT | GDBF_WEIGHT | GDBF_SATURATE,
@@ -62,13 +63,16 @@ GDBF_VARIANTS = {
     "ATGDBF": GDBF_ADAPT,
     "SATGDBF": GDBF_ADAPT | GDBF_SMOOTH,
     "SMGDBF": GDBF_SMOOTH,
+    "SGDBF": GDBF_SEQUENTIAL,
+    "MGDBF": GDBF_MODESWITCH,
+    "StochasticNGDBF": GDBF_QUANTIZE | GDBF_QPROB | GDBF_WEIGHT | GDBF_SATURATE,
 }
 
 
 class _GdbfCfg(C.Structure):
     _fields_ = [("flags", C.c_int32), ("precision", C.c_int32), ("T", C.c_int32), ("windowsize", C.c_int32),
-                ("nq", C.c_int32), ("reserved", C.c_int32), ("theta", C.c_double), ("lambda_", C.c_double),
-                ("alpha", C.c_double), ("noise_scale", C.c_double), ("ymax", C.c_double)]
+                ("nq", C.c_int32), ("tswitch", C.c_int32), ("theta", C.c_double), ("lambda_", C.c_double),
+                ("alpha", C.c_double), ("noise_scale", C.c_double), ("ymax", C.c_double), ("qsigma", C.c_double)]
 
 
 @dataclass
@@ -84,10 +88,12 @@ class GdbfConfig:
     windowsize: int = 16
     nq: int = 16
     precision: int = 0   # F32
+    tswitch: int = 0     # MODESWITCH: Tswitch (:51)
+    qsigma: float = 0.0  # QPROB, gdbf_decode only: the normalCDF sigma
 
     def _c(self) -> _GdbfCfg:
-        return _GdbfCfg(self.flags, self.precision, self.T, self.windowsize, self.nq, 0, self.theta, self.lambda_,
-                        self.alpha, self.noise_scale, self.ymax)
+        return _GdbfCfg(self.flags, self.precision, self.T, self.windowsize, self.nq, self.tswitch, self.theta,
+                        self.lambda_, self.alpha, self.noise_scale, self.ymax, self.qsigma)
 
 
 @dataclass

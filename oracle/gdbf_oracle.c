@@ -14,8 +14,20 @@
  *                       checks are not satisfied (:348-367, :371-375)
  *   saturateSamples     |yq| > Ymax -> yq *= Ymax/|yq| (:255-258)
  *   quantizeSamples     quantize() with NQ levels (:265-267, :488-493)
- * Not restated: modeswitching / sequentialmode (single-bit flips, mu = 0) and
- * quantizeProbabilities (decodeStochasticNGDBF) -- no product counterpart.
+ * and the flip schedules of the other three targets:
+ *   sequentialmode      mu = 0: only the first bit of minimal energy flips
+ *                       (E < Emin from +inf in index order, :573-580, :619-620)
+ *   modeswitching       mu = 1 until, after Tswitch, the objective
+ *                       f = sum d*yq + sum s (:623-632, s as checked) before
+ *                       the bit update is >= the one after it; then mu = 0
+ *                       (:309-311, :338-345)
+ *   quantizeProbabilities  flip with probability pcdf = normalCDF((theta - E) /
+ *                       noiseSigma) rounded to the nearest of 8 levels, by
+ *                       ranu() < level (:562-597); the ranu() draws are the
+ *                       caller's pert rows
+ * (decodeSGDBF = sequentialmode, decodeMGDBF = modeswitching,
+ * decodeStochasticNGDBF = quantizeSamples|quantizeProbabilities|weightSyndromes|
+ * saturateSamples, Makefile:24-31).
  * Build: oracle/Makefile (plain IEEE, -ffp-contract=off).
  */
 #include "ldpc_oracle.h"
@@ -63,6 +75,41 @@ float orc_gdbf_front_f32(float y, const orc_gdbf_cfg *cfg, int *r)
  * d (in: r, out: decisions), pert [T][N] (may be NULL without addNoise; row
  * `it` is used by iteration it), returns the iterations run (`it` after the
  * loop, :399) and sets *satisfied (:300-306). */
+/* The 8 flipping probabilities of quantizeProbabilities (:564-573) and the nearest
+ * one to pcdf by squared distance, first minimum (:574-585). */
+static const double kPrLevels[8] = {0, 0.0625, 0.125, 0.25, 0.34375, 0.4106, 0.68359, 1};
+static double nearest_level(double pcdf)
+{
+    double min_dist = 1;
+    int min_idx = 0;
+    for (int j = 0; j < 8; j++) {
+        double t = kPrLevels[j] - pcdf;
+        t = t * t;
+        if (t < min_dist) {
+            min_dist = t;
+            min_idx = j;
+        }
+    }
+    return kPrLevels[min_idx];
+}
+static float nearest_level_f32(float pcdf)
+{
+    float min_dist = 1;
+    int min_idx = 0;
+    for (int j = 0; j < 8; j++) {
+        float t = (float)kPrLevels[j] - pcdf;
+        t = t * t;
+        if (t < min_dist) {
+            min_dist = t;
+            min_idx = j;
+        }
+    }
+    return (float)kPrLevels[min_idx];
+}
+/* normalCDF (:66-69): 0.5 * erfc(-x * M_SQRT1_2) */
+static double ncdf_f64(double x) { return 0.5 * erfc(-x * 0.70710678118654752440); }
+static float ncdf_f32(float x) { return 0.5f * erfcf(-x * 0.70710678118654752440f); }
+
 #define ORC_DEFINE_GDBF(FT, SUFFIX)                                                     \
 int orc_gdbf_decode_##SUFFIX(const orc_alist *H, const FT *yq, const FT *pert,         \
                              const orc_gdbf_cfg *cfg, int8_t *d, int *satisfied)        \
@@ -75,6 +122,9 @@ int orc_gdbf_decode_##SUFFIX(const orc_alist *H, const FT *yq, const FT *pert,  
     const FT lambda = (FT)cfg->lambda;                                                  \
     for (int i = 0; i < N; ++i) theta[i] = (FT)cfg->theta;                 /* :291-294 */ \
     int it, sat = 0;                                                                    \
+    int mu = (cfg->flags & ORC_GDBF_SEQUENTIAL) ? 0 : 1;                   /* :284-289 */ \
+    const int modesw = (cfg->flags & ORC_GDBF_MODESWITCH) != 0;                         \
+    const FT qsig = (FT)cfg->qsigma;                                                    \
     for (it = 0; it < T; ++it) {                                                        \
         sat = 1;                                                                        \
         for (int j = 0; j < M; ++j) {                          /* :517-534 */           \
@@ -84,14 +134,44 @@ int orc_gdbf_decode_##SUFFIX(const orc_alist *H, const FT *yq, const FT *pert,  
             s[j] = prod;                                                                \
         }                                                                               \
         if (sat) break;                                        /* :305-306 */           \
-        for (int i = 0; i < N; ++i) {                          /* :536-621, mu = 1 */   \
+        FT f1 = 0;                                                                      \
+        if (modesw && it > cfg->tswitch) {                     /* :309-311, :623-632 */ \
+            for (int i = 0; i < N; ++i) f1 += (FT)d[i] * yq[i];                         \
+            for (int j = 0; j < M; ++j) f1 += (FT)s[j];                                 \
+        }                                                                               \
+        FT Emin = (FT)INFINITY;                                                         \
+        int mindx = -1;                                                                 \
+        for (int i = 0; i < N; ++i) {                          /* :536-621 */           \
+            int flip = 0;                                                               \
             FT E = (FT)d[i] * yq[i];                                                    \
             for (int k = 0; k < H->deg_n[i]; ++k)                                       \
                 E += w * (FT)s[H->nlist[(long)i * H->maxdv + k] - 1];                   \
             if (cfg->flags & ORC_GDBF_NOISE) E += pert[(long)it * N + i];               \
-            const int flip = E < theta[i];                                              \
-            if (flip) d[i] = (int8_t)-d[i];                                             \
+            if (cfg->flags & ORC_GDBF_QPROB) {                 /* :562-597 */           \
+                const FT lev = ORC_GDBF_LEVEL_##SUFFIX(ORC_GDBF_NCDF_##SUFFIX((-E + theta[i]) / qsig)); \
+                if (pert[(long)it * N + i] < lev) {                                     \
+                    flip = 1;                                                           \
+                    d[i] = (int8_t)-d[i];                                               \
+                }                                                                       \
+            } else {                                                                    \
+                if (mu == 1 && E < theta[i]) {                 /* :598-603 */           \
+                    flip = 1;                                                           \
+                    d[i] = (int8_t)-d[i];                                               \
+                }                                                                       \
+                if (mu == 0 && E < Emin) {                     /* :604-610 */           \
+                    flip = 1;                                                           \
+                    Emin = E;                                                           \
+                    mindx = i;                                                          \
+                }                                                                       \
+            }                                                                           \
             if ((cfg->flags & ORC_GDBF_ADAPT) && !flip) theta[i] *= lambda;             \
+        }                                                                               \
+        if (mu == 0 && mindx >= 0) d[mindx] = (int8_t)-d[mindx];   /* :619-620 */       \
+        if (modesw && it > cfg->tswitch) {                     /* :338-345 */           \
+            FT f2 = 0;                                                                  \
+            for (int i = 0; i < N; ++i) f2 += (FT)d[i] * yq[i];                         \
+            for (int j = 0; j < M; ++j) f2 += (FT)s[j];                                 \
+            if (f1 >= f2) mu = 0;                                                       \
         }                                                                               \
         if ((cfg->flags & ORC_GDBF_SMOOTH) && it > T - cfg->windowsize)  /* :348-354 */ \
             for (int i = 0; i < N; ++i) dsum[i] += d[i];                                \
@@ -103,6 +183,10 @@ int orc_gdbf_decode_##SUFFIX(const orc_alist *H, const FT *yq, const FT *pert,  
     return it;                                                                          \
 }
 
+#define ORC_GDBF_LEVEL_f64 nearest_level
+#define ORC_GDBF_LEVEL_f32 nearest_level_f32
+#define ORC_GDBF_NCDF_f64 ncdf_f64
+#define ORC_GDBF_NCDF_f32 ncdf_f32
 ORC_DEFINE_GDBF(double, f64)
 ORC_DEFINE_GDBF(float, f32)
 
@@ -146,11 +230,17 @@ int64_t orc_gdbf_run(const orc_alist *H, double R, double snr, const orc_gdbf_cf
          * generator, decode, then advance the real one by the `it` rows used. */
         int it, sat = 0;
         orc_rng g2 = g;
+        orc_gdbf_cfg c2 = *cfg;
+        c2.qsigma = noise_sigma;                               /* symNodeUpdates' sigma (:296, :353) */
         if (cfg->flags & ORC_GDBF_NOISE)
             for (long k = 0; k < (long)N * T; ++k) pert[k] = noise_sigma * orc_rann(&g2);
-        it = orc_gdbf_decode_f64(H, yq, pert, cfg, d, &sat);
+        if (cfg->flags & ORC_GDBF_QPROB)                       /* one ranu() per bit and iteration (:588) */
+            for (long k = 0; k < (long)N * T; ++k) pert[k] = orc_ranu(&g2);
+        it = orc_gdbf_decode_f64(H, yq, pert, &c2, d, &sat);
         if (cfg->flags & ORC_GDBF_NOISE)
             for (long k = 0; k < (long)N * it; ++k) (void)orc_rann(&g);
+        if (cfg->flags & ORC_GDBF_QPROB)
+            for (long k = 0; k < (long)N * it; ++k) (void)orc_ranu(&g);
         if ((cfg->flags & ORC_GDBF_SMOOTH) && it > T - cfg->windowsize) ++*smoothing_used;   /* :371-375 */
         int w = 0;
         for (int i = 0; i < N; ++i) w += d[i] != c[i];         /* :378 */

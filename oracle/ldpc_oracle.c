@@ -50,6 +50,11 @@ double orc_ranf(orc_rng *g)
     return (double)orc_random(g) / (1.0 + (double)0x7fffffff);
 }
 
+double orc_ranu(orc_rng *g)
+{
+    return (1.0 + (double)orc_random(g)) / (2.0 + (double)0x7fffffff);
+}
+
 /* rann(): cos(2*3.141592654*ranf()) * sqrt(-2*log(1-ranf())) (rand.h:19-20).
  * g++ evaluates the cos operand's ranf() first (verified against the
  * reference binary: tests/test_oracle.py::test_rann_kat). */

@@ -114,12 +114,20 @@ enum {
     ORC_GDBF_WEIGHT = 4,     /* -D weightSyndromes     */
     ORC_GDBF_SMOOTH = 8,     /* -D outputSmoothing     */
     ORC_GDBF_SATURATE = 16,  /* -D saturateSamples     */
-    ORC_GDBF_QUANTIZE = 32   /* -D quantizeSamples     */
+    ORC_GDBF_QUANTIZE = 32,  /* -D quantizeSamples     */
+    ORC_GDBF_SEQUENTIAL = 64,   /* -D sequentialmode: mu = 0 from the start          */
+    ORC_GDBF_MODESWITCH = 128,  /* -D modeswitching: mu -> 0 once f1 >= f2 (:309-345) */
+    ORC_GDBF_QPROB = 256        /* -D quantizeProbabilities: stochastic flips (:562-597);
+                                   pert[it][i] then holds the ranu() draws           */
 };
 typedef struct {
     int    flags, T, windowsize, nq;
     double theta, lambda, alpha, noise_scale, ymax;
+    int    tswitch;      /* Tswitch (:51, 0 in the reference)                       */
+    double qsigma;       /* quantizeProbabilities: the sigma of normalCDF (noiseSigma) */
 } orc_gdbf_cfg;
+/* ranu() (rand.h:13-14): (1 + random()) / (2 + 0x7fffffff) */
+double orc_ranu(orc_rng *g);
 /* channel front-end of one sample (:254-267): returns yq, *r = hard decision */
 double orc_gdbf_front(double y, const orc_gdbf_cfg *cfg, int *r);
 float  orc_gdbf_front_f32(float y, const orc_gdbf_cfg *cfg, int *r);

@@ -39,7 +39,8 @@ class _Cfg(C.Structure):
 class _GdbfCfg(C.Structure):
     _fields_ = [("flags", C.c_int), ("T", C.c_int), ("windowsize", C.c_int), ("nq", C.c_int),
                 ("theta", C.c_double), ("lambda_", C.c_double), ("alpha", C.c_double),
-                ("noise_scale", C.c_double), ("ymax", C.c_double)]
+                ("noise_scale", C.c_double), ("ymax", C.c_double), ("tswitch", C.c_int),
+                ("qsigma", C.c_double)]
 
 
 class _Stats(C.Structure):
@@ -59,6 +60,8 @@ def lib():
         L.orc_random.restype = C.c_int32
         L.orc_ranf.argtypes = [C.POINTER(_Rng)]
         L.orc_ranf.restype = C.c_double
+        L.orc_ranu.argtypes = [C.POINTER(_Rng)]
+        L.orc_ranu.restype = C.c_double
         L.orc_rann.argtypes = [C.POINTER(_Rng)]
         L.orc_rann.restype = C.c_double
         L.orc_rann_fill.argtypes = [C.POINTER(_Rng), C.c_long, C.c_double, C.c_void_p]
@@ -124,6 +127,11 @@ class GlibcRandom:
     def rann(self) -> float:
         return lib().orc_rann(C.byref(self._s))
 
+    def ranu_fill(self, n: int) -> np.ndarray:
+        """n draws of rand.h's ranu() = (1 + random()) / (2 + 0x7fffffff)."""
+        f = lib().orc_ranu
+        return np.array([f(C.byref(self._s)) for _ in range(n)], dtype=np.float64)
+
     def rann_fill(self, n: int, scale: float = 1.0) -> np.ndarray:
         out = np.empty(n, dtype=np.float64)
         lib().orc_rann_fill(C.byref(self._s), n, scale, out.ctypes.data)
@@ -157,6 +165,7 @@ class Cfg:
 
 
 GDBF_NOISE, GDBF_ADAPT, GDBF_WEIGHT, GDBF_SMOOTH, GDBF_SATURATE, GDBF_QUANTIZE = 1, 2, 4, 8, 16, 32
+GDBF_SEQUENTIAL, GDBF_MODESWITCH, GDBF_QPROB = 64, 128, 256
 
 
 @dataclass
@@ -171,10 +180,12 @@ class GdbfCfg:
     ymax: float = 0.0
     windowsize: int = 64
     nq: int = 16
+    tswitch: int = 0        # modeswitching: Tswitch (:51)
+    qsigma: float = 0.0     # quantizeProbabilities (gdbf_decode): the sigma of normalCDF
 
     def c(self) -> _GdbfCfg:
         return _GdbfCfg(self.flags, self.T, self.windowsize, self.nq, self.theta, self.lambda_, self.alpha,
-                        self.noise_scale, self.ymax)
+                        self.noise_scale, self.ymax, self.tswitch, self.qsigma)
 
 
 class Alist:

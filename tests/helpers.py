@@ -45,6 +45,9 @@ GDBF_BINARIES = {
     "decodeATGDBF": ("adapt",),
     "decodeSATGDBF": ("adapt", "smooth"),
     "decodeSMGDBF": ("smooth",),
+    "decodeSGDBF": ("sequential",),                                     # Makefile:27-28
+    "decodeMGDBF": ("modeswitch",),                                     # Makefile:24-25
+    "decodeStochasticNGDBF": ("quantize", "qprob", "weight", "saturate"),   # Makefile:30-31
 }
 
 
@@ -58,14 +61,15 @@ def gdbf_config(run):
     rest = a[5:]
     sw = GDBF_BINARIES[run["binary"]]
     bits = {"noise": O.GDBF_NOISE, "adapt": O.GDBF_ADAPT, "weight": O.GDBF_WEIGHT,
-            "smooth": O.GDBF_SMOOTH, "saturate": O.GDBF_SATURATE}
+            "smooth": O.GDBF_SMOOTH, "saturate": O.GDBF_SATURATE, "quantize": O.GDBF_QUANTIZE,
+            "sequential": O.GDBF_SEQUENTIAL, "modeswitch": O.GDBF_MODESWITCH, "qprob": O.GDBF_QPROB}
     cfg = dict(flags=sum(bits[s] for s in sw), T=T, theta=theta, lambda_=0.991, alpha=2.25,
-               noise_scale=1.0, ymax=2.25, windowsize=64)   # the reference's defaults (:48-56)
+               noise_scale=1.0, ymax=2.25, windowsize=64, nq=16)   # the reference's defaults (:48-56)
     i = 0
-    for name, key, conv in (("noise", "noise_scale", float), ("adapt", "lambda_", float),
-                            ("weight", "alpha", float), ("smooth", "windowsize", int),
-                            ("saturate", "ymax", float)):
-        if name in sw:
+    for names, key, conv in ((("noise", "qprob"), "noise_scale", float), (("quantize",), "nq", int),
+                             (("adapt",), "lambda_", float), (("weight",), "alpha", float),
+                             (("smooth",), "windowsize", int), (("saturate",), "ymax", float)):
+        if any(n in sw for n in names):
             cfg[key] = conv(rest[i])
             i += 1
     return R, snr, cfg

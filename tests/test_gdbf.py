@@ -1,9 +1,10 @@
 """GDBF / NGDBF bit flipping (BASELINE config 4).
 
-Oracle tier (CPU): oracle/gdbf_oracle.c restates src/decodeGDBF.cpp in its
-parallel-flip mode and must reproduce every golden reference run
-(tests/golden/reference_runs.json, decodeMNGDBF / decodeSMNGDBF /
-decodeATGDBF / decodeSATGDBF / decodeSMGDBF compiled from the unmodified
+Oracle tier (CPU): oracle/gdbf_oracle.c restates src/decodeGDBF.cpp (parallel,
+sequential and mode-switching flips, stochastic quantised-probability flips)
+and must reproduce every golden reference run (tests/golden/reference_runs.json,
+decodeMNGDBF / decodeSMNGDBF / decodeATGDBF / decodeSATGDBF / decodeSMGDBF /
+decodeSGDBF / decodeMGDBF / decodeStochasticNGDBF compiled from the unmodified
 sources by oracle/Makefile.ref): totals, per-frame error weights, average
 iterations and the log line's smoothing count.
 GPU tier: the HIP kernel through the C ABI, given the reference's own channel
@@ -52,15 +53,24 @@ def _reference_frames(A, run, nframes):
         pert = None
         if cfg.flags & O.GDBF_NOISE:
             pert = g.copy().rann_fill(A.N * cfg.T, sigma * cfg.noise_scale).reshape(cfg.T, A.N)
+        if cfg.flags & O.GDBF_QPROB:
+            pert = g.copy().ranu_fill(A.N * cfg.T).reshape(cfg.T, A.N)
+            cfg.qsigma = sigma * cfg.noise_scale
         d, it, sat = A.gdbf_decode(y, pert, cfg)
         if cfg.flags & O.GDBF_NOISE:
             g.rann_fill(A.N * it)
+        if cfg.flags & O.GDBF_QPROB:
+            g.ranu_fill(A.N * it)
         frames.append((y, pert, d, it, sat, cw))
     return cfg, frames
 
 
-def test_oracle_frame_decode_matches_run():
-    run = [r for r in golden_runs("gdbf") if r["name"] == "smngdbf_peg_3.5_T100_s5"][0]
+@pytest.mark.parametrize("name", ["smngdbf_peg_3.5_T100_s5", "sgdbf_peg_5.0_T100_s5", "mgdbf_peg_4.0_T100_s5",
+                                  "stngdbf_peg_4.0_T100_s5"])
+def test_oracle_frame_decode_matches_run(name):
+    """The one-frame decode (gdbf_decode, the GPU tests' checker) against the frame
+    loop (gdbf_run, pinned to the reference's runs) on the same glibc draws."""
+    run = [r for r in golden_runs("gdbf") if r["name"] == name][0]
     A = O.Alist(code_path(run["code"]))
     R, snr, c = gdbf_config(run)
     n, st, fw, fi = A.gdbf_run(R, snr, O.GdbfCfg(**c), run["seed"], max_frames=6, cap=6)
@@ -77,6 +87,11 @@ GPU_VARIANTS = {
     "SATGDBF": dict(flags=O.GDBF_ADAPT | O.GDBF_SMOOTH),
     "QSMNGDBF": dict(flags=O.GDBF_NOISE | O.GDBF_ADAPT | O.GDBF_WEIGHT | O.GDBF_SMOOTH | O.GDBF_SATURATE
                      | O.GDBF_QUANTIZE, nq=5),
+    "SGDBF": dict(flags=O.GDBF_SEQUENTIAL),
+    "MGDBF": dict(flags=O.GDBF_MODESWITCH),
+    "SMGDBF_MS": dict(flags=O.GDBF_MODESWITCH | O.GDBF_SMOOTH | O.GDBF_NOISE),
+    "StochasticNGDBF": dict(flags=O.GDBF_QUANTIZE | O.GDBF_QPROB | O.GDBF_WEIGHT | O.GDBF_SATURATE, nq=8,
+                            noise_scale=0.9),
 }
 COMMON = dict(T=60, theta=-0.6, lambda_=0.99, alpha=0.8, noise_scale=0.75, ymax=2.5, windowsize=16)
 
@@ -84,7 +99,8 @@ COMMON = dict(T=60, theta=-0.6, lambda_=0.99, alpha=0.8, noise_scale=0.75, ymax=
 def _gpu_cfg(native, c, f32):
     return native.GdbfConfig(flags=c["flags"], T=c["T"], theta=c["theta"], lambda_=c["lambda_"], alpha=c["alpha"],
                              noise_scale=c["noise_scale"], ymax=c["ymax"], windowsize=c["windowsize"],
-                             nq=c.get("nq", 16), precision=native.F32 if f32 else native.F64)
+                             nq=c.get("nq", 16), precision=native.F32 if f32 else native.F64,
+                             tswitch=c.get("tswitch", 0), qsigma=c.get("qsigma", 0.0))
 
 
 @pytest.mark.gpu
@@ -103,11 +119,16 @@ def test_gdbf_decisions_bit_exact_vs_oracle(gpu_ctx_factory, code, vname, prec):
     B = 6
     sigma = math.sqrt(10 ** (-3.0 / 10) / 0.5 / 2)
     y = np.stack([g.channel(np.ones(A.N, dtype=np.int32), sigma) for _ in range(B)]).astype(dt)
-    pert = g.rann_fill(B * cfg.T * A.N, sigma * cfg.noise_scale).reshape(B, cfg.T, A.N).astype(dt)
-    d, fr, cnt = ctx.gdbf_decode(y, pert if cfg.flags & O.GDBF_NOISE else None, _gpu_cfg(native, c, f32))
+    if cfg.flags & O.GDBF_QPROB:   # the ranu() draws of the stochastic flips
+        pert = g.ranu_fill(B * cfg.T * A.N).reshape(B, cfg.T, A.N).astype(dt)
+        c["qsigma"] = cfg.qsigma = sigma * cfg.noise_scale
+    else:
+        pert = g.rann_fill(B * cfg.T * A.N, sigma * cfg.noise_scale).reshape(B, cfg.T, A.N).astype(dt)
+    use_pert = cfg.flags & (O.GDBF_NOISE | O.GDBF_QPROB)
+    d, fr, cnt = ctx.gdbf_decode(y, pert if use_pert else None, _gpu_cfg(native, c, f32))
     its = []
     for b in range(B):
-        want, it, sat = A.gdbf_decode(y[b], pert[b] if cfg.flags & O.GDBF_NOISE else None, cfg)
+        want, it, sat = A.gdbf_decode(y[b], pert[b] if use_pert else None, cfg)
         assert int((d[b] != want).sum()) == 0, b
         assert fr["iters"][b] == it and fr["bit_err"][b] == int((want != 1).sum())
         its.append(it)
@@ -139,10 +160,15 @@ def test_gpu_reproduces_reference_gdbf_run(gpu_ctx_factory, run):
         pert = None
         if cfg.flags & O.GDBF_NOISE:
             pert = g.copy().rann_fill(N * cfg.T, sigma * cfg.noise_scale).reshape(1, cfg.T, N)
+        if cfg.flags & O.GDBF_QPROB:
+            pert = g.copy().ranu_fill(N * cfg.T).reshape(1, cfg.T, N)
+            gcfg.qsigma = sigma * cfg.noise_scale
         _, fr, _ = ctx.gdbf_decode(y[None], pert, gcfg, c=cw.astype(np.int8)[None], want_decisions=False)
         it = int(fr["iters"][0])
         if cfg.flags & O.GDBF_NOISE:
             g.rann_fill(N * it)
+        if cfg.flags & O.GDBF_QPROB:
+            g.ranu_fill(N * it)
         unc += int(fr["uncoded_bit_err"][0])
         iters += it
         if fr["bit_err"][0] > 0:
@@ -184,3 +210,20 @@ def test_gdbf_sim_independent_of_batch_split(gpu_ctx_factory):
     a, _ = ctx.gdbf_sim_batch(3.0, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=100)
     b, _ = ctx.gdbf_sim_batch(3.0, 0.5, cfg, seed=5, stream_id=0, first_cw=100, batch=200)
     assert np.array_equal(full, np.concatenate([a, b]))
+
+
+def test_unsupported_flag_combinations_are_rejected():
+    """ADAPT with single-bit flips and NOISE with QPROB have no reference target; the
+    ABI refuses them instead of guessing (checked before any device call)."""
+    import ctypes
+    from ldpcsimulation_amd import native
+    L = native.lib()
+
+    def rc_of(flags):
+        name = ctypes.create_string_buffer(32)
+        return L.ldpc_gdbf_kernel_info(None, ctypes.byref(native.GdbfConfig(flags=flags)._c()), name, 32, None)
+    for flags in (native.GDBF_ADAPT | native.GDBF_SEQUENTIAL, native.GDBF_ADAPT | native.GDBF_MODESWITCH,
+                  native.GDBF_NOISE | native.GDBF_QPROB):
+        assert rc_of(flags) == -4   # LDPC_ERR_UNSUPPORTED
+    assert rc_of(1024) == -1 and b"unknown GDBF flags" in L.ldpc_last_error()
+    assert rc_of(native.GDBF_VARIANTS["StochasticNGDBF"]) == -1 and b"ctx is null" in L.ldpc_last_error()
