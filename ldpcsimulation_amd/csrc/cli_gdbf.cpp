@@ -355,7 +355,7 @@ int main(int argc, char *argv[])
     const char tab = '\t';
     of << SNR << tab << (double)errors / totalBits << tab << (double)totalIterations / totalWords << tab
        << (double)wordErrors / totalWords << tab << totalBits << tab << totalWords << tab << T << tab << theta << tab;
-#if defined(addNoise)
+#if defined(addNoise) || defined(quantizeProbabilities)
     of << cfg.noise_scale << tab;
 #endif
 #ifdef quantizeSamples
