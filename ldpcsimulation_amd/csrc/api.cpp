@@ -519,6 +519,15 @@ static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool 
            ldpc::redo_lds_bytes(c->dg, f64) <= 160 * 1024;
 }
 
+// Flooding of codes beyond LDS: one launch per phase over an Infinity-Cache-
+// resident set (LDPC_FLOOD_MODE=phase) or the persistent workgroup-per-codeword
+// kernel (default).
+static bool use_flood_phase()
+{
+    const char *e = std::getenv("LDPC_FLOOD_MODE");
+    return e && std::strcmp(e, "phase") == 0;
+}
+
 static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int schedule)
 {
     const ldpc::KernelChoice kc = select_kernel(c, f64, schedule, a.variant);
@@ -527,7 +536,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         int gblocks = 0;
         if (kc.scratch_per_block) {
             gblocks = std::min(a.batch, 4 * c->num_cus);
-            HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks));
+            HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks + 4096));   // + the phase kernels' counters
         }
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
         HIP_TRY(ldpc::bp_launch(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream));
@@ -552,7 +561,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         if (per_cu <= 0) per_cu = 1;
         gblocks = per_cu * c->num_cus;
         if (gblocks > a.batch) gblocks = a.batch;
-        HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks));
+        HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks + 4096));   // + the phase kernels' counters
     }
 #ifdef LDPC_STAMPS
     // diagnostic builds: per-block phase cycle sums appended to $LDPC_STAMPS
@@ -577,8 +586,10 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, kc.lds_bytes, (unsigned *)c->redo.p, c->stream,
                                        c->num_cus));
         HIP_TRY(ldpc::launch_redo(c->dg, a, f64, (const unsigned *)c->redo.p, c->stream, c->num_cus));
-    } else if (layered)
+    } else if (layered) {
         HIP_TRY(ldpc::launch_layered(c->dg, a, f64, kc, c->fs, c->ls, c->gscratch.p, gblocks, c->stream));
+    } else if (kc.name[0] == 'f' && use_flood_phase())
+        HIP_TRY(ldpc::launch_flood_phase(c->dg, c->fs, a, f64, kc, c->gscratch.p, c->gscratch.n, c->stream));
     else
         HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream,
                                     c->has_rs ? &c->rs : nullptr, c->num_cus, c->has_fs ? &c->fs : nullptr));

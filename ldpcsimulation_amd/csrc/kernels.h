@@ -88,6 +88,10 @@ hipError_t launch_decode(const DevGraph &g, const DecodeArgs &a, bool f64, const
                          void *gscratch, int gscratch_blocks, hipStream_t s, const RowSched *rs = nullptr,
                          int num_cus = 256, const FloodSched *fs = nullptr);
 int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc);
+// Flooding of codes beyond LDS as one launch per phase over an Infinity-Cache-
+// resident set of codewords (kernels.hip k_flood_*); gscratch as for "flood".
+hipError_t launch_flood_phase(const DevGraph &g, const FloodSched &fs, const DecodeArgs &a, bool f64,
+                              const KernelChoice &kc, void *gscratch, size_t gscratch_bytes, hipStream_t s);
 
 // Layered schedule (k_decode_layered_*): state in LDS when it fits
 // ("layered_lds"), else in a global slot per block ("layered_global").

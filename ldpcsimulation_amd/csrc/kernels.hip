@@ -470,6 +470,290 @@ static size_t flood_slot_bytes(const DevGraph &g, const FloodSched &fs, bool f64
 }
 
 // =====================================================================
+// Phase-per-launch flooding (codes beyond LDS; LDPC_FLOOD_MODE=phase).
+//
+// The same per-codeword state slots, arithmetic and storage order as
+// k_decode_flood, but the resident set is sized to stay inside the 256 MiB
+// Infinity Cache (K codewords, K * slot_bytes ~ 192 MB) and every phase is
+// its own launch over all K codewords: init (channel), T x {check, bit},
+// finish (decisions, accounting). A launch boundary is the flooding
+// barrier, so a codeword is no longer confined to one workgroup: one thread
+// per row (check) or per bit position (bit) of every resident codeword, the
+// whole GPU on each phase, with no spin-waits. Grid (blocks of the phase,
+// K); slot r of the launch holds codeword b0 + r.
+// =====================================================================
+struct FloodSlot {
+    template <typename F> struct View {
+        F *app, *yq, *c2v;
+        typename F2T<F>::T *m12;
+        uint32_t *meta;
+    };
+    template <typename F>
+    static __device__ __forceinline__ View<F> at(unsigned char *scratch, size_t slot_bytes, int r, const FloodSched &fs)
+    {
+        using F2 = typename F2T<F>::T;
+        View<F> v;
+        const int NP = fs.ngroups * 64;
+        unsigned char *base = scratch + slot_bytes * (size_t)r;
+        v.app = reinterpret_cast<F *>(base);
+        v.yq = v.app + (NP + 1);
+        v.c2v = v.yq + NP;
+        v.m12 = reinterpret_cast<F2 *>(v.c2v + (fs.e_pad + 64 + 1) / 2 * 2);
+        v.meta = reinterpret_cast<uint32_t *>(v.m12 + fs.M_pad);
+        return v;
+    }
+};
+
+template <typename F, int SRC>
+__global__ __launch_bounds__(256) void k_flood_init(DecodeArgs a, DevGraph g, FloodSched fs, unsigned char *scratch,
+                                                    size_t slot_bytes, int b0, int *unc_out)
+{
+    const int r = blockIdx.y, b = b0 + r;
+    if (b >= a.batch) return;
+    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
+    const int N = g.N, NP = fs.ngroups * 64, MP = fs.M_pad;
+    const uint64_t cw = a.first_cw + (uint64_t)b;
+    const int8_t *cvec = nullptr;
+    if (SRC == SRC_GIVEN) {
+        if (a.c) cvec = a.c + (size_t)b * N;
+    } else if (a.cw_table) {
+        cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+    }
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    int unc = 0;
+    if (t * 4 < N) {   // ---- channel + front-end (:214-238) into storage order ----
+        F yv[4];
+        if (SRC == SRC_GIVEN) {
+            const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) yv[q] = (t * 4 + q < N) ? y[t * 4 + q] : F(1);
+        } else {
+            uint32_t u[4];
+            philox4x32_10((uint32_t)t, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, (uint32_t)a.seed,
+                          (uint32_t)(a.seed >> 32), u);
+            F n[4];
+            box_muller(u[0], u[1], n[0], n[1]);
+            box_muller(u[2], u[3], n[2], n[3]);
+            const F sigma = (F)a.sigma;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int v = t * 4 + q;
+                yv[q] = (F)(v < N && cvec ? cvec[v] : 1) * (F(1) + sigma * n[q]);
+                if (v < N && a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv[q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int v = t * 4 + q;
+            if (v < N) {
+                const F q2 = front_end<F>(yv[q], a);
+                const int p = fs.pos_of_bit[v];
+                S.yq[p] = q2;
+                S.app[p] = q2;
+                const int cv = cvec ? cvec[v] : 1;
+                unc += ((q2 > F(0) ? 1 : -1) * cv < 0);
+            }
+        }
+    }
+    for (int i = t; i < MP; i += gridDim.x * blockDim.x) {   // c2v_old = +0 (:364-370)
+        typename F2T<F>::T z;
+        z.x = F(0);
+        z.y = F(0);
+        S.m12[i] = z;
+        S.meta[i] = 0;
+    }
+    if (t == 0) S.app[NP] = dinf<F>();   // sentinel position of padding slots
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) unc += __shfl_xor(unc, o, 64);
+    if ((threadIdx.x & 63) == 0 && unc) atomicAdd(&unc_out[r], unc);
+}
+
+template <typename F, int DC>
+__global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs, unsigned char *scratch,
+                                                     size_t slot_bytes, int nres)
+{
+    using F2 = typename F2T<F>::T;
+    const int r = blockIdx.y;
+    if (r >= nres) return;
+    const int MP = fs.M_pad, NP = fs.ngroups * 64;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= MP) return;
+    const int deg = fs.rdeg[i];
+    if (deg == 0) return;
+    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
+    const F alpha = (F)a.alpha, delta = (F)a.delta;
+    int sp[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) sp[k] = k < deg ? fs.sp[(size_t)k * MP + i] : NP;
+    F xa[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) xa[k] = S.app[sp[k]];
+    const F2 old = S.m12[i];
+    const uint32_t om = S.meta[i];
+    // ---- the check node of k_decode_flood (:410-450, :494-515) ----
+    const int oidx = (int)(om & 31u);
+    F mn1 = dinf<F>(), mn2 = dinf<F>();
+    int amin = 31;
+    uint32_t sg = 0;
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k < deg) {
+            F cold = (k == oidx) ? old.y : old.x;
+            if ((om >> (5 + k)) & 1u) cold = -cold;
+            const F x = xa[k] - cold;                     // v2c (:469)
+            sg |= (uint32_t)(!(x >= F(0))) << k;          // sgn(v2c) < 0 (:518-523)
+            const F ax = dabs(x);
+            if (ax <= mn1) { mn2 = mn1; mn1 = ax; amin = k; }   // :428-433
+            else if (ax < mn2) { mn2 = ax; }                    // :434-437
+        }
+    }
+    const uint32_t degmask = (1u << deg) - 1u;
+    uint32_t eff = (__popc(sg) & 1) ? (sg ^ degmask) : sg;   // prod * sgn(v2c_k)
+    F M1 = mn1, M2 = mn2;
+    if (a.variant == V_NMS) {
+        M1 = nms_div<F>(mn1, alpha, a);               // :498
+        M2 = nms_div<F>(mn2, alpha, a);
+    } else if (a.variant == V_OMS) {
+        const F t1 = mn1 - delta, t2 = mn2 - delta;   // :509
+        const bool p1 = t1 > F(0), p2 = t2 > F(0);
+        M1 = p1 ? t1 : F(0);
+        M2 = p2 ? t2 : F(0);
+        const uint32_t abit = (amin < 31) ? (1u << amin) : 0u;   // sgn(-0.0) = +1 (:511-513)
+        if (!p1 || mn1 == F(0)) eff &= abit;
+        if (!p2 || mn2 == F(0)) eff &= ~abit;
+    }
+    F2 nw;
+    nw.x = M1;
+    nw.y = M2;
+    S.m12[i] = nw;
+    S.meta[i] = (uint32_t)amin | (eff << 5);
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        if (k < deg) {
+            const F mag = (k == amin) ? M2 : M1;
+            S.c2v[fs.sq[(size_t)k * MP + i]] = ((eff >> k) & 1u) ? -mag : mag;
+        }
+    }
+}
+
+template <typename F>
+__global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char *scratch, size_t slot_bytes, int nres)
+{
+    const int r = blockIdx.y;
+    if (r >= nres) return;
+    const int NP = fs.ngroups * 64;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= NP) return;
+    const int d = fs.pdeg[p];
+    if (d == 0) return;
+    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
+    const F *cp = S.c2v + fs.gbase[p >> 6] + (p & 63);
+    F sum = S.yq[p];
+    for (int e = 0; e < d; ++e) sum += cp[64 * e];   // nlist order (:452-476)
+    S.app[p] = sum;
+}
+
+template <typename F>
+__global__ __launch_bounds__(512) void k_flood_finish(DecodeArgs a, DevGraph g, FloodSched fs, unsigned char *scratch,
+                                                      size_t slot_bytes, int b0, const int *unc_in)
+{
+    __shared__ int red[32 + 16 * 8];
+    const int r = blockIdx.x, b = b0 + r;
+    if (b >= a.batch) return;
+    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
+    const int tid = threadIdx.x, nt = blockDim.x, N = g.N, MP = fs.M_pad;
+    const uint64_t cw = a.first_cw + (uint64_t)b;
+    const int8_t *cvec = nullptr;
+    if (a.src == SRC_GIVEN) {
+        if (a.c) cvec = a.c + (size_t)b * N;
+    } else if (a.cw_table) {
+        cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+    }
+    // ---- decisions, error weight (:270, :382-393), syndrome ----
+    int w = 0, synd = 0;
+    for (int v = tid; v < N; v += nt) {
+        const int d = S.app[fs.pos_of_bit[v]] > F(0) ? 1 : -1;   // :471-474
+        const int cv = cvec ? cvec[v] : 1;
+        w += (d != cv);
+        if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+    }
+    for (int i = tid; i < MP; i += nt) {
+        const int deg = fs.rdeg[i];
+        int par = 0;
+        for (int k = 0; k < deg; ++k) par ^= (S.app[fs.sp[(size_t)k * MP + i]] > F(0)) ? 0 : 1;
+        synd |= par;
+    }
+    int sums[3] = {w, 0, synd};
+    block_sum_n<3>(sums, red + 32);
+    if (tid == 0) {
+        const int sf = sums[2] > 0, uc = unc_in[r];
+        atomicAdd(&a.counts[0], (unsigned long long)sums[0]);
+        atomicAdd(&a.counts[1], (unsigned long long)(sums[0] > 0));
+        atomicAdd(&a.counts[2], (unsigned long long)uc);
+        atomicAdd(&a.counts[3], 1ull);
+        atomicAdd(&a.counts[4], (unsigned long long)a.T);
+        atomicAdd(&a.counts[5], (unsigned long long)sf);
+        if (sums[0] > 0 && a.hist) atomicAdd(&a.hist[sums[0] - 1], 1ull);
+        if (a.frame_res) a.frame_res[b] = make_int4(sums[0], uc, sf, 0);
+    }
+}
+
+// Resident codewords of the phase-per-launch flooding: their state fits the
+// Infinity Cache (LDPC_FLOOD_RESIDENT overrides).
+static int flood_phase_resident(size_t slot_bytes, size_t gscratch_bytes)
+{
+    long k = (long)((192ull << 20) / slot_bytes);
+    if (const char *e = std::getenv("LDPC_FLOOD_RESIDENT")) k = std::atol(e);
+    const long cap = (long)((gscratch_bytes - 4096) / slot_bytes);
+    if (k > cap) k = cap;
+    return k < 1 ? 1 : (int)k;
+}
+
+template <typename F, int SRC>
+static hipError_t launch_flood_phase_t(const DevGraph &g, const FloodSched &fs, const DecodeArgs &a,
+                                       const KernelChoice &kc, void *gs, size_t gs_bytes, hipStream_t s)
+{
+    const size_t sb = kc.scratch_per_block;
+    const int K = flood_phase_resident(sb, gs_bytes);
+    unsigned char *scratch = (unsigned char *)gs;
+    int *unc = reinterpret_cast<int *>(scratch + sb * (size_t)K);   // K counters after the slots
+    const int NP = fs.ngroups * 64;
+    for (int b0 = 0; b0 < a.batch; b0 += K) {
+        const int nres = a.batch - b0 < K ? a.batch - b0 : K;
+        hipError_t e = hipMemsetAsync(unc, 0, sizeof(int) * (size_t)nres, s);
+        if (e != hipSuccess) return e;
+        const int ib = ((g.N + 3) / 4 + 255) / 256;
+        hipLaunchKernelGGL((k_flood_init<F, SRC>), dim3(ib > 1 ? ib : 1, nres), dim3(256), 0, s, a, g, fs, scratch, sb,
+                           b0, unc);
+        const dim3 cg((fs.M_pad + 255) / 256, nres), bg((NP + 255) / 256, nres);
+        for (int it = 0; it < a.T; ++it) {
+            if (fs.dc <= 8)
+                hipLaunchKernelGGL((k_flood_check<F, 8>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
+            else if (fs.dc <= 16)
+                hipLaunchKernelGGL((k_flood_check<F, 16>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
+            else
+                hipLaunchKernelGGL((k_flood_check<F, 32>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
+            hipLaunchKernelGGL((k_flood_bit<F>), bg, dim3(256), 0, s, fs, scratch, sb, nres);
+        }
+        hipLaunchKernelGGL((k_flood_finish<F>), dim3(nres), dim3(512), 0, s, a, g, fs, scratch, sb, b0, unc);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_flood_phase(const DevGraph &g, const FloodSched &fs, const DecodeArgs &a, bool f64,
+                              const KernelChoice &kc, void *gscratch, size_t gscratch_bytes, hipStream_t s)
+{
+    if (a.batch <= 0) return hipSuccess;
+    if (f64)
+        return a.src == SRC_GIVEN ? launch_flood_phase_t<double, SRC_GIVEN>(g, fs, a, kc, gscratch, gscratch_bytes, s)
+                                  : launch_flood_phase_t<double, SRC_PHILOX>(g, fs, a, kc, gscratch, gscratch_bytes, s);
+    return a.src == SRC_GIVEN ? launch_flood_phase_t<float, SRC_GIVEN>(g, fs, a, kc, gscratch, gscratch_bytes, s)
+                              : launch_flood_phase_t<float, SRC_PHILOX>(g, fs, a, kc, gscratch, gscratch_bytes, s);
+}
+
+// =====================================================================
 // Layered (row-serial) min-sum -- SURVEY §8(f) row 2, BASELINE config 3.
 // The reference only floods (src/decodeMinSum.cpp:247-263); this is the
 // row-serial schedule of the same check-node rule (:410-450, :494-515),
