@@ -520,12 +520,12 @@ static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool 
 }
 
 // Flooding of codes beyond LDS: one launch per phase over an Infinity-Cache-
-// resident set (LDPC_FLOOD_MODE=phase) or the persistent workgroup-per-codeword
-// kernel (default).
+// resident set (default; 1.5x the persistent kernel on DVB-S2) or the
+// persistent workgroup-per-codeword kernel (LDPC_FLOOD_MODE=persistent).
 static bool use_flood_phase()
 {
     const char *e = std::getenv("LDPC_FLOOD_MODE");
-    return e && std::strcmp(e, "phase") == 0;
+    return !(e && std::strcmp(e, "persistent") == 0);
 }
 
 static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int schedule)
@@ -536,7 +536,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         int gblocks = 0;
         if (kc.scratch_per_block) {
             gblocks = std::min(a.batch, 4 * c->num_cus);
-            HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks + 4096));   // + the phase kernels' counters
+            HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks + 65536));   // + the phase kernels' counters
         }
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
         HIP_TRY(ldpc::bp_launch(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream));
@@ -561,7 +561,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         if (per_cu <= 0) per_cu = 1;
         gblocks = per_cu * c->num_cus;
         if (gblocks > a.batch) gblocks = a.batch;
-        HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks + 4096));   // + the phase kernels' counters
+        HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks + 65536));   // + the phase kernels' counters
     }
 #ifdef LDPC_STAMPS
     // diagnostic builds: per-block phase cycle sums appended to $LDPC_STAMPS

@@ -470,11 +470,12 @@ static size_t flood_slot_bytes(const DevGraph &g, const FloodSched &fs, bool f64
 }
 
 // =====================================================================
-// Phase-per-launch flooding (codes beyond LDS; LDPC_FLOOD_MODE=phase).
+// Phase-per-launch flooding (codes beyond LDS; the default since round 2,
+// LDPC_FLOOD_MODE=persistent selects k_decode_flood).
 //
 // The same per-codeword state slots, arithmetic and storage order as
 // k_decode_flood, but the resident set is sized to stay inside the 256 MiB
-// Infinity Cache (K codewords, K * slot_bytes ~ 192 MB) and every phase is
+// Infinity Cache (K codewords, K * slot_bytes ~ 150 MB) and every phase is
 // its own launch over all K codewords: init (channel), T x {check, bit},
 // finish (decisions, accounting). A launch boundary is the flooding
 // barrier, so a codeword is no longer confined to one workgroup: one thread
@@ -568,23 +569,31 @@ __global__ __launch_bounds__(256) void k_flood_init(DecodeArgs a, DevGraph g, Fl
     if ((threadIdx.x & 63) == 0 && unc) atomicAdd(&unc_out[r], unc);
 }
 
+#ifndef LDPC_FLOOD_CPW
+#define LDPC_FLOOD_CPW 8
+#endif
+// Codewords per thread of the phase kernels: the row's (or bit position's)
+// schedule is loaded once and used for CPW resident codewords (slots
+// blockIdx.y + j * gridDim.y).
 template <typename F, int DC>
 __global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs, unsigned char *scratch,
                                                      size_t slot_bytes, int nres)
 {
     using F2 = typename F2T<F>::T;
-    const int r = blockIdx.y;
-    if (r >= nres) return;
     const int MP = fs.M_pad, NP = fs.ngroups * 64;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= MP) return;
     const int deg = fs.rdeg[i];
     if (deg == 0) return;
-    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
     const F alpha = (F)a.alpha, delta = (F)a.delta;
-    int sp[DC];
+    int sp[DC], sq[DC];
 #pragma unroll
-    for (int k = 0; k < DC; ++k) sp[k] = k < deg ? fs.sp[(size_t)k * MP + i] : NP;
+    for (int k = 0; k < DC; ++k) {
+        sp[k] = k < deg ? fs.sp[(size_t)k * MP + i] : NP;
+        sq[k] = k < deg ? fs.sq[(size_t)k * MP + i] : 0;
+    }
+    for (int r = blockIdx.y; r < nres; r += gridDim.y) {
+    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
     F xa[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) xa[k] = S.app[sp[k]];
@@ -631,80 +640,98 @@ __global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs
     for (int k = 0; k < DC; ++k) {
         if (k < deg) {
             const F mag = (k == amin) ? M2 : M1;
-            S.c2v[fs.sq[(size_t)k * MP + i]] = ((eff >> k) & 1u) ? -mag : mag;
+            S.c2v[sq[k]] = ((eff >> k) & 1u) ? -mag : mag;
         }
+    }
     }
 }
 
 template <typename F>
 __global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char *scratch, size_t slot_bytes, int nres)
 {
-    const int r = blockIdx.y;
-    if (r >= nres) return;
     const int NP = fs.ngroups * 64;
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= NP) return;
     const int d = fs.pdeg[p];
     if (d == 0) return;
-    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
-    const F *cp = S.c2v + fs.gbase[p >> 6] + (p & 63);
-    F sum = S.yq[p];
-    for (int e = 0; e < d; ++e) sum += cp[64 * e];   // nlist order (:452-476)
-    S.app[p] = sum;
+    const int off = fs.gbase[p >> 6] + (p & 63);
+    for (int r = blockIdx.y; r < nres; r += gridDim.y) {
+        const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
+        const F *cp = S.c2v + off;
+        F sum = S.yq[p];
+        for (int e = 0; e < d; ++e) sum += cp[64 * e];   // nlist order (:452-476)
+        S.app[p] = sum;
+    }
 }
 
+// Decisions, error weight (:270, :382-393) and syndrome of every resident
+// codeword: one thread per bit / row, per-slot sums by atomics.
 template <typename F>
-__global__ __launch_bounds__(512) void k_flood_finish(DecodeArgs a, DevGraph g, FloodSched fs, unsigned char *scratch,
-                                                      size_t slot_bytes, int b0, const int *unc_in)
+__global__ __launch_bounds__(256) void k_flood_finish(DecodeArgs a, DevGraph g, FloodSched fs, unsigned char *scratch,
+                                                      size_t slot_bytes, int b0, int nres, int *wsum, int *ssum)
 {
-    __shared__ int red[32 + 16 * 8];
-    const int r = blockIdx.x, b = b0 + r;
-    if (b >= a.batch) return;
-    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
-    const int tid = threadIdx.x, nt = blockDim.x, N = g.N, MP = fs.M_pad;
-    const uint64_t cw = a.first_cw + (uint64_t)b;
-    const int8_t *cvec = nullptr;
-    if (a.src == SRC_GIVEN) {
-        if (a.c) cvec = a.c + (size_t)b * N;
-    } else if (a.cw_table) {
-        cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+    const int N = g.N, MP = fs.M_pad;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int r = blockIdx.y; r < nres; r += gridDim.y) {
+        const int b = b0 + r;
+        const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
+        int w = 0, par = 0;
+        if (t < N) {
+            const uint64_t cw = a.first_cw + (uint64_t)b;
+            const int8_t *cvec = nullptr;
+            if (a.src == SRC_GIVEN) {
+                if (a.c) cvec = a.c + (size_t)b * N;
+            } else if (a.cw_table) {
+                cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+            }
+            const int d = S.app[fs.pos_of_bit[t]] > F(0) ? 1 : -1;   // :471-474
+            w = d != (cvec ? cvec[t] : 1);
+            if (a.d_out) a.d_out[(size_t)b * N + t] = (int8_t)d;
+        }
+        if (t < MP) {
+            const int deg = fs.rdeg[t];
+            for (int k = 0; k < deg; ++k) par ^= (S.app[fs.sp[(size_t)k * MP + t]] > F(0)) ? 0 : 1;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            w += __shfl_xor(w, o, 64);
+            par += __shfl_xor(par, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (w) atomicAdd(&wsum[r], w);
+            if (par) atomicAdd(&ssum[r], par);
+        }
     }
-    // ---- decisions, error weight (:270, :382-393), syndrome ----
-    int w = 0, synd = 0;
-    for (int v = tid; v < N; v += nt) {
-        const int d = S.app[fs.pos_of_bit[v]] > F(0) ? 1 : -1;   // :471-474
-        const int cv = cvec ? cvec[v] : 1;
-        w += (d != cv);
-        if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
-    }
-    for (int i = tid; i < MP; i += nt) {
-        const int deg = fs.rdeg[i];
-        int par = 0;
-        for (int k = 0; k < deg; ++k) par ^= (S.app[fs.sp[(size_t)k * MP + i]] > F(0)) ? 0 : 1;
-        synd |= par;
-    }
-    int sums[3] = {w, 0, synd};
-    block_sum_n<3>(sums, red + 32);
-    if (tid == 0) {
-        const int sf = sums[2] > 0, uc = unc_in[r];
-        atomicAdd(&a.counts[0], (unsigned long long)sums[0]);
-        atomicAdd(&a.counts[1], (unsigned long long)(sums[0] > 0));
-        atomicAdd(&a.counts[2], (unsigned long long)uc);
-        atomicAdd(&a.counts[3], 1ull);
-        atomicAdd(&a.counts[4], (unsigned long long)a.T);
-        atomicAdd(&a.counts[5], (unsigned long long)sf);
-        if (sums[0] > 0 && a.hist) atomicAdd(&a.hist[sums[0] - 1], 1ull);
-        if (a.frame_res) a.frame_res[b] = make_int4(sums[0], uc, sf, 0);
-    }
+}
+
+// The frame accounting of the resident codewords (one thread per slot).
+__global__ __launch_bounds__(256) void k_flood_account(DecodeArgs a, int b0, int nres, const int *unc,
+                                                       const int *wsum, const int *ssum)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nres) return;
+    const int b = b0 + r, w = wsum[r], uc = unc[r], sf = ssum[r] > 0;
+    atomicAdd(&a.counts[0], (unsigned long long)w);
+    atomicAdd(&a.counts[1], (unsigned long long)(w > 0));
+    atomicAdd(&a.counts[2], (unsigned long long)uc);
+    atomicAdd(&a.counts[3], 1ull);
+    atomicAdd(&a.counts[4], (unsigned long long)a.T);
+    atomicAdd(&a.counts[5], (unsigned long long)sf);
+    if (w > 0 && a.hist) atomicAdd(&a.hist[w - 1], 1ull);
+    if (a.frame_res) a.frame_res[b] = make_int4(w, uc, sf, 0);
 }
 
 // Resident codewords of the phase-per-launch flooding: their state fits the
 // Infinity Cache (LDPC_FLOOD_RESIDENT overrides).
+constexpr size_t kFloodPhaseExtra = 65536;   // per-slot counters after the slots (3 ints per slot)
 static int flood_phase_resident(size_t slot_bytes, size_t gscratch_bytes)
 {
-    long k = (long)((192ull << 20) / slot_bytes);
+    // 150 MB of state: 128 DVB-S2 codewords. At 192 MB (164) the rate fell by a
+    // fifth on some boxes and not on others -- the edge of what stays resident.
+    long k = (long)((150ull << 20) / slot_bytes);
     if (const char *e = std::getenv("LDPC_FLOOD_RESIDENT")) k = std::atol(e);
-    const long cap = (long)((gscratch_bytes - 4096) / slot_bytes);
+    if (k > 4096) k = 4096;
+    const long cap = (long)((gscratch_bytes - kFloodPhaseExtra) / slot_bytes);
     if (k > cap) k = cap;
     return k < 1 ? 1 : (int)k;
 }
@@ -716,16 +743,18 @@ static hipError_t launch_flood_phase_t(const DevGraph &g, const FloodSched &fs, 
     const size_t sb = kc.scratch_per_block;
     const int K = flood_phase_resident(sb, gs_bytes);
     unsigned char *scratch = (unsigned char *)gs;
-    int *unc = reinterpret_cast<int *>(scratch + sb * (size_t)K);   // K counters after the slots
+    int *unc = reinterpret_cast<int *>(scratch + sb * (size_t)K);   // per-slot counters after the slots
+    int *wsum = unc + K, *ssum = wsum + K;
     const int NP = fs.ngroups * 64;
     for (int b0 = 0; b0 < a.batch; b0 += K) {
         const int nres = a.batch - b0 < K ? a.batch - b0 : K;
-        hipError_t e = hipMemsetAsync(unc, 0, sizeof(int) * (size_t)nres, s);
+        hipError_t e = hipMemsetAsync(unc, 0, sizeof(int) * 3 * (size_t)K, s);
         if (e != hipSuccess) return e;
         const int ib = ((g.N + 3) / 4 + 255) / 256;
         hipLaunchKernelGGL((k_flood_init<F, SRC>), dim3(ib > 1 ? ib : 1, nres), dim3(256), 0, s, a, g, fs, scratch, sb,
                            b0, unc);
-        const dim3 cg((fs.M_pad + 255) / 256, nres), bg((NP + 255) / 256, nres);
+        const int gy = (nres + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW;
+        const dim3 cg((fs.M_pad + 255) / 256, gy), bg((NP + 255) / 256, gy);
         for (int it = 0; it < a.T; ++it) {
             if (fs.dc <= 8)
                 hipLaunchKernelGGL((k_flood_check<F, 8>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
@@ -735,7 +764,10 @@ static hipError_t launch_flood_phase_t(const DevGraph &g, const FloodSched &fs, 
                 hipLaunchKernelGGL((k_flood_check<F, 32>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
             hipLaunchKernelGGL((k_flood_bit<F>), bg, dim3(256), 0, s, fs, scratch, sb, nres);
         }
-        hipLaunchKernelGGL((k_flood_finish<F>), dim3(nres), dim3(512), 0, s, a, g, fs, scratch, sb, b0, unc);
+        const int fx = ((g.N > fs.M_pad ? g.N : fs.M_pad) + 255) / 256;
+        hipLaunchKernelGGL((k_flood_finish<F>), dim3(fx, gy), dim3(256), 0, s, a, g, fs, scratch, sb, b0, nres, wsum,
+                           ssum);
+        hipLaunchKernelGGL(k_flood_account, dim3((nres + 255) / 256), dim3(256), 0, s, a, b0, nres, unc, wsum, ssum);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
