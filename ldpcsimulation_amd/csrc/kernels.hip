@@ -572,6 +572,9 @@ __global__ __launch_bounds__(256) void k_flood_init(DecodeArgs a, DevGraph g, Fl
 #ifndef LDPC_FLOOD_CPW
 #define LDPC_FLOOD_CPW 8
 #endif
+#ifndef LDPC_FLOOD_XCD
+#define LDPC_FLOOD_XCD 1
+#endif
 // Codewords per thread of the phase kernels: the row's (or bit position's)
 // schedule is loaded once and used for CPW resident codewords (slots
 // blockIdx.y + j * gridDim.y).
@@ -581,7 +584,14 @@ __global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs
 {
     using F2 = typename F2T<F>::T;
     const int MP = fs.M_pad, NP = fs.ngroups * 64;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+#if LDPC_FLOOD_XCD
+    // XCD-aware: blocks b and b + 8 share an XCD (round-robin placement, speed
+    // only); XCD x decodes the slots x, x + 8, ... one after the other, all
+    // rows of a slot at once, so the ~3.5 gathers of each app value hit its L2.
+    const int i = (blockIdx.x >> 3) * blockDim.x + threadIdx.x, r0 = blockIdx.x & 7, rs = 8;
+#else
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, r0 = blockIdx.y, rs = gridDim.y;
+#endif
     if (i >= MP) return;
     const int deg = fs.rdeg[i];
     if (deg == 0) return;
@@ -592,7 +602,7 @@ __global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs
         sp[k] = k < deg ? fs.sp[(size_t)k * MP + i] : NP;
         sq[k] = k < deg ? fs.sq[(size_t)k * MP + i] : 0;
     }
-    for (int r = blockIdx.y; r < nres; r += gridDim.y) {
+    for (int r = r0; r < nres; r += rs) {
     const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
     F xa[DC];
 #pragma unroll
@@ -650,12 +660,16 @@ template <typename F>
 __global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char *scratch, size_t slot_bytes, int nres)
 {
     const int NP = fs.ngroups * 64;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+#if LDPC_FLOOD_XCD
+    const int p = (blockIdx.x >> 3) * blockDim.x + threadIdx.x, r0 = blockIdx.x & 7, rs = 8;
+#else
+    const int p = blockIdx.x * blockDim.x + threadIdx.x, r0 = blockIdx.y, rs = gridDim.y;
+#endif
     if (p >= NP) return;
     const int d = fs.pdeg[p];
     if (d == 0) return;
     const int off = fs.gbase[p >> 6] + (p & 63);
-    for (int r = blockIdx.y; r < nres; r += gridDim.y) {
+    for (int r = r0; r < nres; r += rs) {
         const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
         const F *cp = S.c2v + off;
         F sum = S.yq[p];
@@ -754,7 +768,11 @@ static hipError_t launch_flood_phase_t(const DevGraph &g, const FloodSched &fs, 
         hipLaunchKernelGGL((k_flood_init<F, SRC>), dim3(ib > 1 ? ib : 1, nres), dim3(256), 0, s, a, g, fs, scratch, sb,
                            b0, unc);
         const int gy = (nres + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW;
+#if LDPC_FLOOD_XCD
+        const dim3 cg(8 * ((fs.M_pad + 255) / 256)), bg(8 * ((NP + 255) / 256));
+#else
         const dim3 cg((fs.M_pad + 255) / 256, gy), bg((NP + 255) / 256, gy);
+#endif
         for (int it = 0; it < a.T; ++it) {
             if (fs.dc <= 8)
                 hipLaunchKernelGGL((k_flood_check<F, 8>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
