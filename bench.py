@@ -21,7 +21,9 @@ the same steps and reported under "f32".
 process, before anything touches the GPU) and exits with its status.
 
 Prints ONE JSON line (rank 0). value = decoded coded bits per second over all
-ranks (Mbit/s), max-over-ranks wall time of the K timed steps.
+ranks (Mbit/s), max-over-ranks wall time of the K timed steps. With N > 1 each
+step also all-reduces that round's per-frame counter sums over the ranks (RCCL,
+on the launch stream), the exchange the sharded SNR driver makes per round.
 
 roofline: the resource that bounds the row kernel is the LDS
 pipe. `achieved` = the LDS-array cycles the kernel's dataflow issues per
@@ -267,6 +269,11 @@ def main():
         def step(k):
             first = (k * world + rank) * B
             ctx.sim_launch(args.ebn0, 0.5, cfg, args.seed, stream_id, first, B, frames_dev)
+            if world > 1 and args.backend == "nccl":
+                # the sharded driver's per-round exchange (sim.simulate_point): this round's
+                # counters summed over ranks, RCCL on the launch stream
+                part = frames_dev.sum(dim=0, dtype=torch.int64)
+                dist.all_reduce(part)
 
         for k in range(args.warmup):
             step(k)
