@@ -419,26 +419,64 @@ std::string build_layers(const ldpc_graph &g, const FloodSchedule &s, LayerSched
     const int M = g.M, N = g.N;
     if ((int)s.row_of.size() < M) return "flood schedule missing";
     const int dcs = std::max(g.maxdc, 1);
-    // first-fit colouring in chain order
+    // Chain-level first-fit colouring. The flood schedule's row chains (a
+    // quasi-cyclic block row: DVB-S2's 360-row groups) are split where a row
+    // shares a bit with an earlier row of the same piece; each piece joins the
+    // lowest layer none of its bits is in yet. Whole chains per layer keep the
+    // gathers of consecutive lanes on consecutive positions (DVB-S2: 3.2
+    // instead of 11.5 cache lines per 64-lane gather with row-level colouring,
+    // at the same 17 layers). Pieces shorter than 32 rows (codes without
+    // long chains, e.g. PEG) are coloured row by row.
+    std::vector<int32_t> piece_start;
+    {
+        std::vector<int32_t> mark(N, -1);
+        int cur = -1;
+        for (int i = 0; i < M; ++i) {
+            const int j = s.row_of[i];
+            if (j < 0) return "padding inside the row order";
+            const int32_t *rc = &g.row_cols[(size_t)j * dcs];
+            bool clash = false;
+            for (int k = 0; k < g.row_deg[j]; ++k) clash |= cur >= 0 && mark[rc[k]] == cur;
+            if (cur < 0 || clash || (i < (int)s.chain_head.size() && s.chain_head[i])) {
+                piece_start.push_back(i);
+                cur = (int)piece_start.size() - 1;
+            }
+            for (int k = 0; k < g.row_deg[j]; ++k) mark[rc[k]] = cur;
+        }
+        piece_start.push_back(M);
+        // pieces shorter than a wave gain no coalescing: colour their rows one by one
+        std::vector<int32_t> ps;
+        for (size_t c = 0; c + 1 < piece_start.size(); ++c) {
+            if (piece_start[c + 1] - piece_start[c] >= 32) ps.push_back(piece_start[c]);
+            else
+                for (int i = piece_start[c]; i < piece_start[c + 1]; ++i) ps.push_back(i);
+        }
+        ps.push_back(M);
+        piece_start.swap(ps);
+    }
     std::vector<std::vector<int32_t>> bit_layers(N);
     std::vector<int32_t> layer_of(M, -1), forbid;
     int nlayers = 0;
-    for (int i = 0; i < M; ++i) {
-        const int j = s.row_of[i];
-        if (j < 0) return "padding inside the row order";
-        const int32_t *rc = &g.row_cols[(size_t)j * dcs];
+    for (size_t c = 0; c + 1 < piece_start.size(); ++c) {
         forbid.clear();
-        for (int k = 0; k < g.row_deg[j]; ++k)
-            for (int32_t L : bit_layers[rc[k]]) forbid.push_back(L);
+        for (int i = piece_start[c]; i < piece_start[c + 1]; ++i) {
+            const int j = s.row_of[i];
+            const int32_t *rc = &g.row_cols[(size_t)j * dcs];
+            for (int k = 0; k < g.row_deg[j]; ++k)
+                for (int32_t L : bit_layers[rc[k]]) forbid.push_back(L);
+        }
         std::sort(forbid.begin(), forbid.end());
         int L = 0;
         for (int32_t f : forbid) {
             if (f == L) ++L;
             else if (f > L) break;
         }
-        layer_of[i] = L;
         nlayers = std::max(nlayers, L + 1);
-        for (int k = 0; k < g.row_deg[j]; ++k) bit_layers[rc[k]].push_back(L);
+        for (int i = piece_start[c]; i < piece_start[c + 1]; ++i) {
+            layer_of[i] = L;
+            const int j = s.row_of[i];
+            for (int k = 0; k < g.row_deg[j]; ++k) bit_layers[g.row_cols[(size_t)j * dcs + k]].push_back(L);
+        }
     }
     // layered order: layer by layer, chain order inside a layer
     std::vector<int32_t> cnt(nlayers + 1, 0), pos_i(M);

@@ -76,11 +76,12 @@ struct FloodSchedule {
 std::string build_flood_schedule(const ldpc_graph &g, FloodSchedule &s);
 
 // Layered schedule (kernels.hip, k_decode_layered_*): rows grouped into
-// layers of rows that share no bit, by first-fit colouring in the flood
-// schedule's chain order (each row joins the lowest layer none of its bits
-// is in yet), so a quasi-cyclic block row stays together and rows keep
-// their chain neighbours (coalesced gathers). The serial row order is
-// layer by layer, each layer in chain order; updating a layer's rows in
+// layers of rows that share no bit, by first-fit colouring of whole row
+// chains of the flood schedule (each chain -- split where it would share a
+// bit with itself -- joins the lowest layer none of its bits is in yet), so a
+// quasi-cyclic block row stays together and rows keep their chain neighbours
+// (coalesced gathers). The serial row order is layer by layer, each layer in
+// chain order; updating a layer's rows in
 // parallel equals updating them serially in that order (bit-disjoint rows
 // commute), which is the oracle's row-serial definition.
 struct LayerSchedule {

@@ -7,8 +7,8 @@ as the reference's :410-450/:494-515; "parity unpinned" against the
 reference, pinned against that oracle). Bit-exact tier: identical y ->
 identical decisions for every variant, fp32 and fp64.
 
-CPU tests: the layer partition (bit-disjoint row sets by first-fit colouring:
-17 layers on DVB-S2 N=64800, the 12 block rows of Z=81 on 802.11n N=1944) and
+CPU tests: the layer partition (bit-disjoint row sets by first-fit colouring of
+row chains: 17 layers on DVB-S2 N=64800, the 12 block rows of Z=81 on 802.11n N=1944) and
 the commutation property the GPU kernel relies on (any order of the rows
 inside a layer gives the same result). GPU tests: the HIP kernels against the oracle.
 """
@@ -51,7 +51,7 @@ def _frames(N, n, ebn0, seed, dtype=np.float64):
 @pytest.mark.parametrize("code,want", [("dvbs2_1_2.alist", None), ("80211n_1944_r12.alist", (12, 81)),
                                        ("PEGReg504x1008.alist", None)])
 def test_layer_partition_is_bit_disjoint(code, want):
-    """Layers: bit-disjoint row sets (first-fit colouring, graph.cpp build_layers); the
+    """Layers: bit-disjoint row sets (chain-level first-fit colouring, graph.cpp build_layers); the
     802.11n N=1944 code comes out as its 12 block rows of Z=81."""
     from ldpcsimulation_amd import codes
     g, order, ptr = _layers(code)
@@ -63,10 +63,9 @@ def test_layer_partition_is_bit_disjoint(code, want):
         cols = [c for j in order[ptr[L]:ptr[L + 1]] for c in H.rows[j]]
         assert len(cols) == len(set(cols)), f"layer {L} rows share a bit"
         layer_bits.append(set(cols))
-    # first fit: every row of layer L > 0 clashes with some earlier layer's bits
+    # first fit over whole row chains: every layer L > 0 clashes with each earlier layer
     for L in range(1, len(ptr) - 1):
-        for j in order[ptr[L]:ptr[L + 1]][:20]:
-            assert all(set(H.rows[j]) & layer_bits[K] for K in range(L))
+        assert all(layer_bits[L] & layer_bits[K] for K in range(L))
     if want:
         assert (len(ptr) - 1, int(np.diff(ptr).max())) == want
         assert np.all(np.diff(ptr) == want[1])
