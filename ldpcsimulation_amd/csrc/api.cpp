@@ -368,13 +368,17 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
             c->has_fs = true;
             ldpc::LayerSchedule lh;
             if (fh.dc <= ldpc::kPackedMaxDc && ldpc::build_layers(*g, fh, lh).empty()) {
-                const size_t n_lp = lh.lptr.size(), n_sp = lh.sp.size(), n_rd = lh.rdeg.size();
-                const size_t o_sp = al(4 * n_lp), o_rd = o_sp + al(4 * n_sp), tot = o_rd + al(n_rd);
+                const size_t n_lp = lh.lptr.size(), n_sp = lh.sp.size(), n_rd = lh.rdeg.size(),
+                             n_pb = lh.pos_of_bit.size();
+                const size_t o_sp = al(4 * n_lp), o_rd = o_sp + al(4 * n_sp), o_pb = o_rd + al(n_rd),
+                             tot = o_pb + al(4 * n_pb);
                 CTX_TRY(c->lsched.ensure(tot));
                 unsigned char *lb = (unsigned char *)c->lsched.p;
                 CTX_TRY(hipMemcpy(lb, lh.lptr.data(), 4 * n_lp, hipMemcpyHostToDevice));
                 CTX_TRY(hipMemcpy(lb + o_sp, lh.sp.data(), 4 * n_sp, hipMemcpyHostToDevice));
                 CTX_TRY(hipMemcpy(lb + o_rd, lh.rdeg.data(), n_rd, hipMemcpyHostToDevice));
+                CTX_TRY(hipMemcpy(lb + o_pb, lh.pos_of_bit.data(), 4 * n_pb, hipMemcpyHostToDevice));
+                c->ls.pos_of_bit = (const int32_t *)(lb + o_pb);
                 c->ls.nlayers = (int)n_lp - 1;
                 c->ls.M_pad = lh.M_pad;
                 c->ls.lptr = (const int32_t *)lb;

@@ -489,12 +489,20 @@ std::string build_layers(const ldpc_graph &g, const FloodSchedule &s, LayerSched
     const int NP = s.ngroups * 64;
     ls.row_order.assign(M, -1);
     ls.rdeg.assign(ls.M_pad, 0);
+    // positions ranked by degree, high first (stable: chains of equal-degree bits stay consecutive)
+    std::vector<int32_t> by_deg(NP), rank(NP + 1);
+    for (int p = 0; p < NP; ++p) by_deg[p] = p;
+    std::stable_sort(by_deg.begin(), by_deg.end(), [&](int32_t x, int32_t y) { return s.pdeg[x] > s.pdeg[y]; });
+    for (int q = 0; q < NP; ++q) rank[by_deg[q]] = q;
+    rank[NP] = NP;   // the +inf sentinel keeps its place
+    ls.pos_of_bit.resize(N);
+    for (int v = 0; v < N; ++v) ls.pos_of_bit[v] = rank[s.pos_of_bit[v]];
     ls.sp.assign((size_t)ls.dc * ls.M_pad, NP);
     for (int n = 0; n < M; ++n) {
         const int i = pos_i[n];
         ls.row_order[n] = s.row_of[i];
         ls.rdeg[n] = s.rdeg[i];
-        for (int k = 0; k < s.dc; ++k) ls.sp[(size_t)k * ls.M_pad + n] = s.sp[(size_t)k * s.M_pad + i];
+        for (int k = 0; k < s.dc; ++k) ls.sp[(size_t)k * ls.M_pad + n] = rank[s.sp[(size_t)k * s.M_pad + i]];
     }
     return "";
 }

@@ -88,9 +88,12 @@ struct LayerSchedule {
     int M_pad = 0, dc = 0;
     std::vector<int32_t> row_order;   // [M] check row at layered position n
     std::vector<int32_t> lptr;        // [nlayers + 1] layered positions of each layer
-    std::vector<int32_t> sp;          // [dc * M_pad] slot-major storage position (FloodSchedule order) of
-                                      // edge k of the row at layered position n (pads: the +inf sentinel)
+    std::vector<int32_t> sp;          // [dc * M_pad] slot-major layered position of edge k of the row at
+                                      // layered position n (pads: the +inf sentinel, ngroups * 64)
     std::vector<uint8_t> rdeg;        // [M_pad]
+    std::vector<int32_t> pos_of_bit;  // [N] layered position of bit v: the FloodSchedule positions ranked
+                                      // by bit degree (stable), so the most-gathered bits come first --
+                                      // the global kernel keeps positions [0, P) in LDS
 };
 std::string build_layers(const ldpc_graph &g, const FloodSchedule &s, LayerSchedule &ls);
 

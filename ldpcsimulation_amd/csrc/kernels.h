@@ -65,8 +65,9 @@ struct FloodSched {
 struct LayerSched {
     int nlayers = 0, max_layer = 0, M_pad = 0;
     const int32_t *lptr = nullptr;  // [nlayers + 1] layered row positions of each layer
-    const int32_t *sp = nullptr;    // [dc * M_pad] slot-major storage positions (fs order of bits)
+    const int32_t *sp = nullptr;    // [dc * M_pad] slot-major layered positions (graph.h LayerSchedule)
     const uint8_t *rdeg = nullptr;  // [M_pad]
+    const int32_t *pos_of_bit = nullptr;   // [N] layered position of each bit
 };
 
 struct KernelChoice {

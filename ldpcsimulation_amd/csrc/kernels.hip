@@ -809,20 +809,85 @@ hipError_t launch_flood_phase(const DevGraph &g, const FloodSched &fs, const Dec
 // row-serial schedule of the same check-node rule (:410-450, :494-515),
 // restated in oracle/ldpc_oracle.c (orc_decode_layered_*):
 //   x_k = app[b_k] - c2v_old_k;  c2v_k = rule(x);  app[b_k] = x_k + c2v_k
-// row by row in the flood schedule's chain order. Consecutive rows that share
-// no bit commute exactly, so each layer (LayerSched: maximal bit-disjoint runs
-// of chain-order rows; DVB-S2 N=64800: 90 layers of 360 rows) is updated by
-// all its rows at once, one thread per row, with a workgroup barrier between
-// layers. One workgroup per codeword (persistent over the batch). State:
-//   app[NP + 1]            posteriors in storage order (app[NP] = +inf pad)
+// row by row in the layered order. Rows that share no bit commute exactly, so
+// each layer (LayerSched: bit-disjoint sets of whole row chains; DVB-S2
+// N=64800: 17 layers of 275-3 044 rows) is updated by all its rows at once,
+// one thread per row, with a workgroup barrier between layers. One workgroup
+// per codeword (persistent over the batch). State:
+//   app[NP + 1]            posteriors in layered position order (app[NP] = +inf pad)
 //   m12[M_pad], meta[M_pad] the packed check state as in k_decode_flood
 // -- in LDS when it fits (k_decode_layered_lds) or in a per-workgroup global
-// slot (k_decode_layered_global: DVB-S2's 583 KB). No yq and no E-sized
-// message array: a row's old messages are rebuilt from its packed state.
+// slot (k_decode_layered_global: DVB-S2's 583 KB), where in fp64 positions [0, P) --
+// the highest-degree bits, LayerSchedule::pos_of_bit -- stay in LDS (LayApp).
+// No yq and no E-sized message array: a row's old messages are rebuilt from
+// its packed state.
 // =====================================================================
-template <typename F, int SRC>
-__device__ __forceinline__ int channel_to_storage(const DecodeArgs &a, const DevGraph &g, const FloodSched &fs,
-                                                  int b, const int8_t *cvec, F *app)
+// Raw buffer access (32-bit byte offsets from a descriptor). The global half
+// of a split posterior array goes through these: a distinct instruction, so
+// the compiler cannot fold "LDS or global" into one flat load.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(void *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)bytes, 0x00020000);
+}
+template <typename F>
+__device__ __forceinline__ F buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off);
+template <>
+__device__ __forceinline__ float buf_ld<float>(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+template <>
+__device__ __forceinline__ double buf_ld<double>(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    const u2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+    return __hiloint2double((int)v.y, (int)v.x);
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, float x)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, double x)
+{
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    u2 v;
+    v.x = (unsigned)__double2loint(x);
+    v.y = (unsigned)__double2hiint(x);
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, (int)off, 0, 0);
+}
+
+// SPLIT: branch-free -- every access issues both the LDS and the buffer
+// instruction; the side that does not hold p gets LDS slot P (a dummy) or an
+// offset past the descriptor's range (the buffer unit drops it: no traffic).
+template <typename F, bool SPLIT>
+struct LayApp {
+    F *lo;                       // positions [0, P): LDS (all of them unless SPLIT); SPLIT: lo[P] = dummy
+    __amdgpu_buffer_rsrc_t hi;   // positions [P, NP]: the global slot, at p - P (SPLIT only)
+    int P;
+    static constexpr uint32_t kOut = 0x80000000u;   // beyond any slot
+    __device__ __forceinline__ F ld(int p) const
+    {
+        if (!SPLIT) return lo[p];
+        const bool in = p < P;
+        const F a = lo[in ? p : P];
+        const F b = buf_ld<F>(hi, in ? kOut : (uint32_t)(p - P) * (uint32_t)sizeof(F));
+        return in ? a : b;
+    }
+    __device__ __forceinline__ void st(int p, F x) const
+    {
+        if (!SPLIT) {
+            lo[p] = x;
+            return;
+        }
+        const bool in = p < P;
+        lo[in ? p : P] = x;
+        buf_st(hi, in ? kOut : (uint32_t)(p - P) * (uint32_t)sizeof(F), x);
+    }
+};
+
+template <typename F, int SRC, bool SPLIT>
+__device__ __forceinline__ int channel_to_storage(const DecodeArgs &a, const DevGraph &g, const LayerSched &ls,
+                                                  int b, const int8_t *cvec, const LayApp<F, SPLIT> &app)
 {
     const int tid = threadIdx.x, nt = blockDim.x, N = g.N;
     const uint64_t cw = a.first_cw + (uint64_t)b;
@@ -831,7 +896,7 @@ __device__ __forceinline__ int channel_to_storage(const DecodeArgs &a, const Dev
         const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
         for (int v = tid; v < N; v += nt) {
             const F q = front_end<F>(y[v], a);
-            app[fs.pos_of_bit[v]] = q;
+            app.st(ls.pos_of_bit[v], q);
             const int cv = cvec ? cvec[v] : 1;
             unc += ((q > F(0) ? 1 : -1) * cv < 0);
         }
@@ -852,7 +917,7 @@ __device__ __forceinline__ int channel_to_storage(const DecodeArgs &a, const Dev
                     const F yv = (F)cv * (F(1) + sigma * n[q4]);
                     if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
                     const F q = front_end<F>(yv, a);
-                    app[fs.pos_of_bit[v]] = q;
+                    app.st(ls.pos_of_bit[v], q);
                     unc += ((q > F(0) ? 1 : -1) * cv < 0);
                 }
             }
@@ -914,9 +979,9 @@ __device__ __forceinline__ uint32_t layered_row(const DecodeArgs &a, int deg, ty
     return (uint32_t)amin | (eff << 5);
 }
 
-template <typename F, int SRC, int DC, int R>
+template <typename F, int SRC, int DC, int R, bool SPLIT>
 __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const DevGraph &g, const FloodSched &fs,
-                                                  const LayerSched &ls, int b, F *app,
+                                                  const LayerSched &ls, int b, const LayApp<F, SPLIT> &app,
                                                   typename F2T<F>::T *m12, uint32_t *meta, int *red,
                                                   unsigned long long *acc)
 {
@@ -932,7 +997,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
         cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
     }
     // ---- channel + front-end (:214-238): app = yq in storage order ----
-    const int unc = channel_to_storage<F, SRC>(a, g, fs, b, cvec, app);
+    const int unc = channel_to_storage<F, SRC, SPLIT>(a, g, ls, b, cvec, app);
     for (int i = tid; i < MP; i += nt) {   // c2v_old = +0 (:364-370)
         F2 z;
         z.x = F(0);
@@ -961,7 +1026,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) xs[r][k] = app[sp[r][k]];
+                    for (int k = 0; k < DC; ++k) xs[r][k] = app.ld(sp[r][k]);
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     if (deg[r]) {
@@ -978,7 +1043,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
                         meta[i0 + r * nt] = nm;
 #pragma unroll
                         for (int k = 0; k < DC; ++k)
-                            if (k < deg[r]) app[sp[r][k]] = xs[r][k];   // posterior update
+                            if (k < deg[r]) app.st(sp[r][k], xs[r][k]);   // posterior update
                     }
                 }
             }
@@ -989,7 +1054,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
     // ---- decisions, error weight (:270, :382-393), syndrome ----
     int w = 0, synd = 0;
     for (int v = tid; v < N; v += nt) {
-        const int d = app[fs.pos_of_bit[v]] > F(0) ? 1 : -1;   // :471-474
+        const int d = app.ld(ls.pos_of_bit[v]) > F(0) ? 1 : -1;   // :471-474
         const int cv = cvec ? cvec[v] : 1;
         w += (d != cv);
         if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
@@ -997,7 +1062,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
     for (int i = tid; i < MP; i += nt) {
         const int deg = ls.rdeg[i];
         int par = 0;
-        for (int k = 0; k < deg; ++k) par ^= (app[ls.sp[(size_t)k * MP + i]] > F(0)) ? 0 : 1;
+        for (int k = 0; k < deg; ++k) par ^= (app.ld(ls.sp[(size_t)k * MP + i]) > F(0)) ? 0 : 1;
         synd |= par;
     }
     int sums[3] = {w, unc, synd};
@@ -1049,29 +1114,36 @@ __global__ __launch_bounds__(512) void k_decode_layered_lds(DecodeArgs a, DevGra
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
     }
+    const LayApp<F, false> la{app, buf_rsrc(app, 0), 0};
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
-        decode_layered_cw<F, SRC, DC, R>(a, g, fs, ls, b, app, m12, meta, red, acc);
+        decode_layered_cw<F, SRC, DC, R, false>(a, g, fs, ls, b, la, m12, meta, red, acc);
     flush_acc(a, acc);
 }
-
-template <typename F, int SRC, int DC, int R>
+// State in a global slot; SPLIT (fp64): except the posteriors of layered
+// positions [0, P) (dynamic LDS, (P + 1) * sizeof(F) bytes) -- DVB-S2 keeps
+// 19 455 of its 64 800 bits there, every degree-8 bit and a third of the
+// degree-3 ones, 54 % of the edge gathers and scatters.
+template <typename F, int SRC, int DC, int R, bool SPLIT>
 __global__ __launch_bounds__(512) void k_decode_layered_global(DecodeArgs a, DevGraph g, FloodSched fs, LayerSched ls,
-                                                               unsigned char *scratch, size_t slot_bytes)
+                                                               unsigned char *scratch, size_t slot_bytes, int P)
 {
     using F2 = typename F2T<F>::T;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int red[16 * 4];
     __shared__ unsigned long long acc[6];
     unsigned char *base = scratch + slot_bytes * blockIdx.x;
     F *app = reinterpret_cast<F *>(base);
     F2 *m12 = reinterpret_cast<F2 *>(base + layered_m12_off(fs, sizeof(F)));
     uint32_t *meta = reinterpret_cast<uint32_t *>(m12 + ls.M_pad);
+    const LayApp<F, SPLIT> la{SPLIT ? reinterpret_cast<F *>(smem) : app,
+                              buf_rsrc(app, (uint32_t)layered_m12_off(fs, sizeof(F))), P};
     if (threadIdx.x == 0) {
-        app[fs.ngroups * 64] = dinf<F>();
+        la.st(fs.ngroups * 64, dinf<F>());
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
     }
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
-        decode_layered_cw<F, SRC, DC, R>(a, g, fs, ls, b, app, m12, meta, red, acc);
+        decode_layered_cw<F, SRC, DC, R, SPLIT>(a, g, fs, ls, b, la, m12, meta, red, acc);
     flush_acc(a, acc);
 }
 
@@ -1805,9 +1877,24 @@ int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc)
 
 
 // ---------------------------------------------------------------- layered
+// Layered positions (of np) the global kernel keeps in LDS: as many as fit
+// beside the static LDS (LDPC_LAYERED_LDS_POS caps it; 0 = all in the slot).
+static int layered_lds_positions(int np, size_t fsz)
+{
+    long P = (long)((kMaxLds - 4096) / fsz) - 1;
+    if (const char *e = std::getenv("LDPC_LAYERED_LDS_POS")) P = std::min(P, std::max(0L, std::atol(e)));
+    return (int)std::min(P, (long)np);
+}
+
 // Rows per thread per pass: the global kernel batches R rows' gathers
 // (latency of the L2/Infinity Cache), the LDS kernel does one row at a time.
-static int layered_rows_per_pass(bool global, bool f64) { return global ? (f64 ? 1 : 4) : 1; }
+// fp64: 2 (DVB-S2 1 530 vs 1 470 Mbit/s at 1 and 1 425 at 3); LDPC_LAYERED_R64=1 for A/B.
+static int layered_r64()
+{
+    const char *e = std::getenv("LDPC_LAYERED_R64");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+}
+static int layered_rows_per_pass(bool global, bool f64) { return global ? (f64 ? layered_r64() : 4) : 1; }
 
 static int layered_threads(const LayerSched &ls, int R, int cap)
 {
@@ -1852,9 +1939,20 @@ static hipError_t launch_layered_t(const DecodeArgs &a, const DevGraph &g, const
         hipLaunchKernelGGL(fn, dim3(grid), dim3(kc.threads), kc.lds_bytes, s, a, g, fs, ls);
     } else {
         const int grid = gblocks < a.batch ? gblocks : a.batch;
-        constexpr int R = sizeof(F) == 4 ? 4 : 1;   // layered_rows_per_pass(true, f64)
-        hipLaunchKernelGGL((k_decode_layered_global<F, SRC, DC, R>), dim3(grid), dim3(kc.threads), 0, s, a, g, fs, ls,
-                           (unsigned char *)gs, kc.scratch_per_block);
+        // fp64 (R = 2, fewer rows in flight per pass: latency-bound): the posteriors of
+        // the highest-degree bits in LDS (DVB-S2 1 130 -> 1 470 Mbit/s at R = 1); fp32
+        // (R = 4): all in the slot -- the split's dual accesses cost it more (2 230 -> 2 010)
+        constexpr bool SPLIT = sizeof(F) == 8;
+        const int r = layered_rows_per_pass(true, sizeof(F) == 8);
+        decltype(&k_decode_layered_global<F, SRC, DC, 1, SPLIT>) fn;
+        if constexpr (sizeof(F) == 4) fn = k_decode_layered_global<F, SRC, DC, 4, SPLIT>;
+        else fn = r == 2 ? k_decode_layered_global<F, SRC, DC, 2, SPLIT> : k_decode_layered_global<F, SRC, DC, 1, SPLIT>;
+        const int P = SPLIT ? layered_lds_positions(fs.ngroups * 64 + 1, sizeof(F)) : 0;
+        const int lds = SPLIT ? (P + 1) * (int)sizeof(F) : 0;   // + LayApp's dummy slot
+        hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(kc.threads), lds, s, a, g, fs, ls, (unsigned char *)gs,
+                           kc.scratch_per_block, P);
     }
     return hipGetLastError();
 }
@@ -1885,9 +1983,10 @@ hipError_t launch_layered(const DevGraph &g, const DecodeArgs &a, bool f64, cons
 int layered_blocks_per_cu(bool f64, const KernelChoice &kc)
 {
     int nb = 0;
-    const void *fn = f64 ? (const void *)k_decode_layered_global<double, SRC_PHILOX, 8, 1>
-                         : (const void *)k_decode_layered_global<float, SRC_PHILOX, 8, 4>;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads, 0);
+    const void *fn = f64 ? (const void *)k_decode_layered_global<double, SRC_PHILOX, 8, 2, true>
+                         : (const void *)k_decode_layered_global<float, SRC_PHILOX, 8, 4, false>;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads,
+        f64 ? (layered_lds_positions(1 << 30, 8) + 1) * 8 : 0);
     if (e != hipSuccess) { (void)hipGetLastError(); return 0; }
     return nb;
 }
