@@ -515,10 +515,17 @@ static bool is_layered(const ldpc::KernelChoice &kc) { return kc.name[0] == 'l' 
 
 // fp64 row graphs run the fast-path row kernel (rows_fast.hip) plus the exact
 // re-decode of codewords whose premise failed; LDPC_ROWS=old keeps the old one.
-static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64)
+// fp32 keeps the row kernel (its fast->exact hand-over measured 8.78 ms against
+// 10.05 ms for the fp32 pair instance of rows_fast); LDPC_ROWS32=fast
+// selects the latter (MS and verified-reciprocal NMS; a after nms_setup).
+static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
 {
     const char *env = std::getenv("LDPC_ROWS");
     if (env && std::strcmp(env, "old") == 0) return false;
+    if (!f64) {
+        const char *e32 = std::getenv("LDPC_ROWS32");
+        if (!(e32 && std::strcmp(e32, "fast") == 0) || !ldpc::rows_fast_f32_ok(a)) return false;
+    }
     return kc.name[0] == 'r' && c->has_rs && ldpc::rows_fast_supported(c->rs, f64) &&
            ldpc::redo_lds_bytes(c->dg, f64) <= 160 * 1024;
 }
@@ -581,13 +588,13 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
 #endif
     // fp64 row graphs: the fast-path kernel plus the exact re-decode of any
     // codeword whose premise failed (LDPC_ROWS=old keeps the old row kernel).
-    const bool fast = use_rows_fast(c, kc, f64);
+    const bool fast = use_rows_fast(c, kc, f64, a);
     if (fast) HIP_TRY(c->redo.ensure(sizeof(unsigned) * ((size_t)c->max_batch + 1)));
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
     c->last_fast = fast;
     if (fast) {
         HIP_TRY(hipMemsetAsync(c->redo.p, 0, sizeof(unsigned), c->stream));
-        HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, kc.lds_bytes, (unsigned *)c->redo.p, c->stream,
+        HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, f64, kc.lds_bytes, (unsigned *)c->redo.p, c->stream,
                                        c->num_cus));
         HIP_TRY(ldpc::launch_redo(c->dg, a, f64, (const unsigned *)c->redo.p, c->stream, c->num_cus));
     } else if (layered) {
@@ -919,8 +926,12 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     int rc = check_cfg(c, cfg);
     if (rc) return rc;
     const ldpc::KernelChoice kc = select_kernel(c, f64, cfg->schedule, cfg->variant);
+    ldpc::DecodeArgs a;
+    fill_common(a, c, cfg, 1);
+    rc = nms_setup(c, cfg, a);   // fp32 NMS: whether the verified reciprocal (and so the fast kernel) applies
+    if (rc) return rc;
     if (name && name_len > 0)
-        std::snprintf(name, (size_t)name_len, "%s", cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64) ? "rows_fast" : kc.name);
+        std::snprintf(name, (size_t)name_len, "%s", cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64, a) ? "rows_fast" : kc.name);
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
     if (bpc) *bpc = cfg->variant == LDPC_BP ? 0 : is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
                                    : ldpc::blocks_per_cu(c->dg, f64, kc);

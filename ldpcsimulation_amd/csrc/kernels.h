@@ -113,13 +113,16 @@ constexpr int kPackedMaxDc = 26;
 // normalisation divides: |v2c| minima). *mismatches receives the count.
 hipError_t verify_div_by_reciprocal(float alpha, float rcp, unsigned long long *mismatches_dev, hipStream_t s);
 
-// Fast-path row kernel (rows_fast.hip): fp64, same LDS layout and schedule as
-// the "rows" kernel (lds_bytes of its KernelChoice), check node compiled per
-// variant; codeword groups whose premise fails are appended to redo
-// (redo[0] = count, must be 0 at launch; redo[1..] batch indices, capacity
-// batch), and launch_redo (kernels.hip) decodes them on the exact path.
+// Fast-path row kernel (rows_fast.hip): fp64 (one codeword per block) and fp32
+// (a pair, dc <= 8), same LDS layout and schedule as the "rows" kernel
+// (lds_bytes of its KernelChoice), check node compiled per variant; codeword
+// groups whose premise fails are appended to redo (redo[0] = count, must be 0
+// at launch; redo[1..] batch indices, capacity batch), and launch_redo
+// (kernels.hip) decodes them on the exact path. fp32 takes it only for MS and
+// for NMS with the verified reciprocal (rows_fast_f32_ok, after nms_setup).
 bool rows_fast_supported(const RowSched &rs, bool f64);
-hipError_t launch_rows_fast(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, int lds_bytes,
+bool rows_fast_f32_ok(const DecodeArgs &a);
+hipError_t launch_rows_fast(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, bool f64, int lds_bytes,
                             unsigned *redo, hipStream_t s, int num_cus);
 // alpha for which the fast fp64 NMS division x*r + one fma correction is exact
 bool markstein_exact_alpha(double alpha);

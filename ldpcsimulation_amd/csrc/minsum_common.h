@@ -170,4 +170,102 @@ __device__ __forceinline__ void vn_phases(const Pack<F, C> *c2v, const int (&bas
     if constexpr (NACT > 1) vn_phases<F, C, NACT - 1, CPT>(c2v, base, gd, k, sum);
 }
 
+// Check node, fast fp32 path (MS, and NMS with a verified reciprocal). Exact
+// whenever every c2v magnitude entering the iteration is below 1e30: then
+// every app and v2c is finite (|app| <= |yq| + 255*1e30 < FLT_MAX), no NaN
+// occurs, and
+//   m2' = med3(m1, |x|, m2), m1' = min(m1, |x|)
+// is exactly the reference's update (m1 <= m2 always). app is never -0 (yq is
+// canonicalised, see the kernel), so v2c = app - c2v is never -0 either and
+// its sign bit is the reference's sgn(v2c) (:518-523): the row parity is the
+// xor of the v2c bit patterns, and c2v_k = (m1|m2) with sign bit
+// parity ^ sign(v2c_k) (a zero magnitude keeps that sign, as prod*min*sgn
+// does). Padding edges read +inf: sign +, never below m2. The new messages
+// are always committed; the return value is false when one of them reaches
+// 1e30 (or is inf), and the caller hands the block to the exact path before
+// the next iteration (keeping the premise true).
+template <int DC, int C>
+__device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DC], Pack<float, C> (&pv)[DC], bool nms,
+                                        float alpha, float rcp)
+{
+    constexpr uint32_t SIGN = 0x80000000u;
+    using V = float __attribute__((ext_vector_type(C)));   // C = 2: one v_pk_add_f32 per edge
+    V x[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        V xi, pi;
+        __builtin_memcpy(&xi, &xin[k], sizeof(V));
+        __builtin_memcpy(&pi, &pv[k], sizeof(V));
+        x[k] = xi - pi;                                                         // v2c (:469)
+    }
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        // (m1, m2) = the two smallest |v2c| of the row, by groups of three
+        // (lo, sec) = (min3, med3), merged with sec' = med3(lo, lo_g, min(sec, sec_g))
+        // (or, for three groups, min(med3(lo_1..3), min3(sec_1..3))).
+        constexpr int G = (DC + 2) / 3;
+        float lo[G], sec[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int k0 = 3 * g, n = DC - k0 < 3 ? DC - k0 : 3;
+            const float a0 = __builtin_fabsf(x[k0][c]);
+            if (n == 3) {
+                const float a1 = __builtin_fabsf(x[k0 + 1][c]), a2 = __builtin_fabsf(x[k0 + 2][c]);
+                lo[g] = __builtin_fminf(__builtin_fminf(a0, a1), a2);
+                sec[g] = __builtin_amdgcn_fmed3f(a0, a1, a2);
+            } else if (n == 2) {
+                const float a1 = __builtin_fabsf(x[k0 + 1][c]);
+                lo[g] = __builtin_fminf(a0, a1);
+                sec[g] = __builtin_fmaxf(a0, a1);
+            } else {
+                lo[g] = a0;
+                sec[g] = __builtin_huge_valf();
+            }
+        }
+        float mn1, mn2;
+        if constexpr (G == 3) {
+            mn1 = __builtin_fminf(__builtin_fminf(lo[0], lo[1]), lo[2]);
+            mn2 = __builtin_fminf(__builtin_amdgcn_fmed3f(lo[0], lo[1], lo[2]),
+                                  __builtin_fminf(__builtin_fminf(sec[0], sec[1]), sec[2]));
+        } else {
+            mn1 = lo[0];
+            mn2 = sec[0];
+#pragma unroll
+            for (int g = 1; g < G; ++g) {
+                mn2 = __builtin_amdgcn_fmed3f(mn1, lo[g], __builtin_fminf(mn2, sec[g]));
+                mn1 = __builtin_fminf(mn1, lo[g]);
+            }
+        }
+        uint32_t par = 0;
+#pragma unroll
+        for (int k = 0; k + 1 < DC; k += 2)                                   // xor3
+            par = __builtin_amdgcn_bitop3_b32(par, __float_as_uint(x[k][c]), __float_as_uint(x[k + 1][c]), 0x96);
+        if (DC & 1) par ^= __float_as_uint(x[DC - 1][c]);
+        float M1 = mn1, M2 = mn2;
+        if (nms) {   // x/alpha = q + (x - q*alpha)*r, q = x*r (verified for all finite x); inf/alpha = inf
+            const float q1 = mn1 * rcp, q2 = mn2 * rcp;
+            const float d1 = __builtin_fmaf(__builtin_fmaf(-q1, alpha, mn1), rcp, q1);
+            const float d2 = __builtin_fmaf(__builtin_fmaf(-q2, alpha, mn2), rcp, q2);
+            M1 = mn1 < __builtin_huge_valf() ? d1 : mn1;
+            M2 = mn2 < __builtin_huge_valf() ? d2 : mn2;
+        }
+        ok &= M2 < 1e30f;
+        uint32_t s1 = __float_as_uint(M1) ^ (par & SIGN), s2 = __float_as_uint(M2) ^ (par & SIGN);
+        asm("" : "+v"(s1), "+v"(s2));   // keep the parity out of the per-edge select
+        // all compares first (separate lane masks), then the selects: no
+        // compare->select hazard wait states between neighbours
+        bool eq[DC];
+#pragma unroll
+        for (int k = 0; k < DC; ++k) eq[k] = __builtin_fabsf(x[k][c]) == mn1;
+#pragma unroll
+        for (int k = 0; k < DC; ++k) {
+            const uint32_t m = eq[k] ? s2 : s1;
+            // m ^ (v2c_k & SIGN)
+            pv[k].v[c] = __uint_as_float(__builtin_amdgcn_bitop3_b32(m, __float_as_uint(x[k][c]), SIGN, 0x78));
+        }
+    }
+    return ok;
+}
+
 }  // namespace ldpc

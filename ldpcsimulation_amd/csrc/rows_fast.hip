@@ -43,7 +43,11 @@
 //    away from every rounding midpoint -- so the correction rounds to
 //    RN(x/alpha). Valid for 2^-960 <= x < 2^1000 and x = 0;
 //    other minima break the premise.
-// fp32 (C = 2 codewords per block) uses cn_fast of minsum_common.h.
+// fp32 (C = 2 codewords per block, packed as float2) uses cn_fast of
+// minsum_common.h -- MS, and NMS with the device-verified reciprocal -- with
+// its own premise (every |c2v| and |yq| below 1e30). Opt-in (LDPC_ROWS32=fast):
+// bit-exact, but 10.05 ms per bench launch against 8.78 ms for kernels.hip's
+// fp32 row kernel, which stays the fp32 default.
 #include "kernels.h"
 #include "device_common.h"
 #include "minsum_common.h"
@@ -221,7 +225,9 @@ template <typename F, int SRC, int C, int DC, int CPT, int RPT, int VAR, bool FD
 __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_eu) void k_rows_fast(
     DecodeArgs a, DevGraph g, RowSched rs, unsigned *redo)
 {
-    static_assert(sizeof(F) == 8 && C == 1, "fp64 fast kernel");
+    static_assert(sizeof(F) == 8 ? C == 1 : (C == 2 && VAR != V_OMS), "fp64 single / fp32 pair fast kernel");
+    constexpr bool F64 = sizeof(F) == 8;
+    const F kMax = F64 ? (F)kFast64Max : (F)1e30f;   // premise bound on |yq|
     using P = Pack<F, C>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, nt = blockDim.x;
@@ -264,7 +270,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
         app[N] = inf;
     }
     if ((tid >> 6) >= (nt >> 7)) __builtin_amdgcn_s_setprio(1);   // MI355X_MICROARCH item 4
-    const F alpha = (F)a.alpha, delta = (F)a.delta, rcp = (F)(1.0 / a.alpha);
+    const F alpha = (F)a.alpha, delta = (F)a.delta, rcp = F64 ? (F)(1.0 / a.alpha) : (F)a.alpha_rcp;
     const int ngrp = (a.batch + C - 1) / C;
     // the block's totals (thread 0), added to a.counts once at the end; in the
     // dynamic area (no static LDS: app starts at LDS address 0)
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 yq[i].v[c] = st.v[c] + F(0);
-                in_ok &= __builtin_fabs(yq[i].v[c]) < (F)kFast64Max;
+                in_ok &= dabs(yq[i].v[c]) < kMax;
             }
             app[vdst(i)] = yq[i];   // v2c = yq on the first pass (:364-370)
         }
@@ -385,8 +391,10 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                     ok = true;
 #pragma unroll
                     for (int k = 0; k < DC; ++k) prev[r][k].v[0] = xin[r % NB][k].v[0] - prev[r][k].v[0];
-                } else {
+                } else if constexpr (F64) {
                     ok = cn_fast64<DC, VAR, FDIV>(xin[r % NB], prev[r], alpha, rcp, delta);
+                } else {
+                    ok = cn_fast<DC, C>(xin[r % NB], prev[r], VAR == V_NMS, (float)alpha, (float)rcp);
                 }
                 if (!ok && deg[r] > 0) red[31] = 1;   // rows past M (degree 0) only write dummy slots
                 if constexpr (LDPC_FAST_EXP != 1) {
@@ -490,57 +498,68 @@ bool markstein_exact_alpha(double alpha)
     return (sig >> tz) < (1ull << 20);
 }
 
-template <int VAR, bool FDIV, int SRC, int DC, int CPT, int RPT>
+template <typename F, int VAR, bool FDIV, int SRC, int DC, int CPT, int RPT>
 static hipError_t launch_fast_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, int lds, unsigned *redo,
                                 hipStream_t s, int num_cus)
 {
-    auto fn = k_rows_fast<double, SRC, 1, DC, CPT, RPT, VAR, FDIV>;
+    constexpr int C = sizeof(F) == 8 ? 1 : 2;
+    auto fn = k_rows_fast<F, SRC, C, DC, CPT, RPT, VAR, FDIV>;
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     int per_cu = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, rs.threads, lds);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    const int ngrp = (a.batch + C - 1) / C;
     int grid = per_cu * num_cus;
-    if (grid > a.batch) grid = a.batch;
+    if (grid > ngrp) grid = ngrp;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(rs.threads), lds, s, a, g, rs, redo);
     return hipGetLastError();
 }
 
-template <int VAR, bool FDIV, int SRC>
+template <typename F, int VAR, bool FDIV, int SRC>
 static hipError_t launch_fast_shape(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, int lds, unsigned *redo,
                                     hipStream_t s, int num_cus)
 {
 #define LDPC_FAST_CASE(DCV, CPTV, RPTV) \
-    if (rs.dc == DCV && rs.cpt == CPTV && rs.rpt == RPTV) return launch_fast_t<VAR, FDIV, SRC, DCV, CPTV, RPTV>(g, rs, a, lds, redo, s, num_cus);
+    if (rs.dc == DCV && rs.cpt == CPTV && rs.rpt == RPTV) return launch_fast_t<F, VAR, FDIV, SRC, DCV, CPTV, RPTV>(g, rs, a, lds, redo, s, num_cus);
     LDPC_FAST_CASE(8, 4, 2)
     LDPC_FAST_CASE(8, 2, 1)
     LDPC_FAST_CASE(8, 4, 1)
-    LDPC_FAST_CASE(16, 4, 2)
-    LDPC_FAST_CASE(16, 2, 1)
-    LDPC_FAST_CASE(16, 4, 1)
+    if constexpr (sizeof(F) == 8) {   // fp32 rows with dc > 8 hold one codeword per block: the old kernel
+        LDPC_FAST_CASE(16, 4, 2)
+        LDPC_FAST_CASE(16, 2, 1)
+        LDPC_FAST_CASE(16, 4, 1)
+    }
 #undef LDPC_FAST_CASE
     return hipErrorInvalidValue;
 }
 
 bool rows_fast_supported(const RowSched &rs, bool f64)
 {
-    if (!f64 || rs.threads <= 0) return false;
-    if (rs.dc != 8 && rs.dc != 16) return false;
+    if (rs.threads <= 0) return false;
+    if (rs.dc != 8 && !(f64 && rs.dc == 16)) return false;
     return (rs.rpt == 2 && rs.cpt == 4) || (rs.rpt == 1 && (rs.cpt == 2 || rs.cpt == 4));
 }
 
-hipError_t launch_rows_fast(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, int lds_bytes,
+bool rows_fast_f32_ok(const DecodeArgs &a) { return a.variant == V_MS || (a.variant == V_NMS && a.nms_fast); }
+
+hipError_t launch_rows_fast(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, bool f64, int lds_bytes,
                             unsigned *redo, hipStream_t s, int num_cus)
 {
-    const bool fdiv = a.variant == V_NMS && markstein_exact_alpha(a.alpha);
     const bool given = a.src == SRC_GIVEN;
-#define LDPC_FAST_SRC(VARV, FD)                                                                         \
-    return given ? launch_fast_shape<VARV, FD, SRC_GIVEN>(g, rs, a, lds_bytes, redo, s, num_cus)        \
-                 : launch_fast_shape<VARV, FD, SRC_PHILOX>(g, rs, a, lds_bytes, redo, s, num_cus);
-    if (a.variant == V_MS) { LDPC_FAST_SRC(V_MS, false) }
-    if (a.variant == V_OMS) { LDPC_FAST_SRC(V_OMS, false) }
-    if (fdiv) { LDPC_FAST_SRC(V_NMS, true) }
-    LDPC_FAST_SRC(V_NMS, false)
+#define LDPC_FAST_SRC(FT, VARV, FD)                                                                         \
+    return given ? launch_fast_shape<FT, VARV, FD, SRC_GIVEN>(g, rs, a, lds_bytes, redo, s, num_cus)        \
+                 : launch_fast_shape<FT, VARV, FD, SRC_PHILOX>(g, rs, a, lds_bytes, redo, s, num_cus);
+    if (!f64) {   // fp32: MS, or NMS with the verified reciprocal (rows_fast_f32_ok)
+        if (a.variant == V_MS) { LDPC_FAST_SRC(float, V_MS, false) }
+        if (a.variant == V_NMS && a.nms_fast) { LDPC_FAST_SRC(float, V_NMS, true) }
+        return hipErrorInvalidValue;
+    }
+    const bool fdiv = a.variant == V_NMS && markstein_exact_alpha(a.alpha);
+    if (a.variant == V_MS) { LDPC_FAST_SRC(double, V_MS, false) }
+    if (a.variant == V_OMS) { LDPC_FAST_SRC(double, V_OMS, false) }
+    if (fdiv) { LDPC_FAST_SRC(double, V_NMS, true) }
+    LDPC_FAST_SRC(double, V_NMS, false)
 #undef LDPC_FAST_SRC
 }
 

@@ -185,6 +185,9 @@ def test_all_kernels_bit_identical(monkeypatch, code):
         monkeypatch.setenv("LDPC_ROWS", "old")   # the previous row kernel (exact + fast loops in one)
         outs["rows_old"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
         monkeypatch.delenv("LDPC_ROWS", raising=False)
+        monkeypatch.setenv("LDPC_ROWS32", "fast")   # fp32: the pair instance of rows_fast (opt-in)
+        outs["rows_fast32"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
+        monkeypatch.delenv("LDPC_ROWS32", raising=False)
         ref = outs["global"]
         for k, o in outs.items():
             for a, b in zip(o[:3], ref[:3]):

@@ -73,8 +73,20 @@ def test_fast_kernel_is_the_f64_row_kernel(gpu_ctx_factory, code):
     ctx = gpu_ctx_factory(code)
     cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=5, precision=native.F64)
     assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
-    cfg.precision = native.F32
+    cfg.precision = native.F32                       # fp32: the row kernel by default
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
+
+
+@pytest.mark.gpu
+def test_f32_pair_fast_kernel_opt_in(gpu_ctx_factory, monkeypatch):
+    """LDPC_ROWS32=fast selects the fp32 pair instance of rows_fast for MS and
+    verified-reciprocal NMS; OMS keeps the row kernel."""
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory("80211n_1944_r12.alist")
+    monkeypatch.setenv("LDPC_ROWS32", "fast")
+    for v, want in ((native.MS, "rows_fast"), (native.NMS, "rows_fast"), (native.OMS, "rows")):
+        cfg = native.DecoderConfig(variant=v, alpha=1.25, delta=0.1, T=5, precision=native.F32)
+        assert ctx.kernel_info(cfg)["kernel"] == want
 
 
 @pytest.mark.gpu
@@ -115,6 +127,47 @@ def test_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, code, vname, v):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("code", ["80211n_1944_r12.alist", "PEGReg504x1008.alist"])
+@pytest.mark.parametrize("vname,v", [("ms", dict(variant=0)), ("nms", dict(variant=1, alpha=1.25))])
+def test_f32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, code, vname, v):
+    """fp32: frames that break the fast premise (|yq| >= 1e30, inf, NaN, values growing
+    past 1e30 mid-decode) -- the pair instance of rows_fast (LDPC_ROWS32=fast) re-decodes
+    them on the exact path, the row kernel hands them over to its exact loop; both give
+    the fp32 oracle's decisions and counters."""
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(code)
+    monkeypatch.setenv("LDPC_ROWS32", "fast")
+    N = ctx.graph.N
+    y = _glibc_frames(N, 16, 1.5, 0.5, seed=4243).astype(np.float32)
+    y[1] *= np.float32(1e31)          # input premise: |yq| >= 1e30
+    y[3, 5] = np.inf                  # non-finite input
+    y[4, 7] = np.nan
+    y[5] *= np.float32(2.0 ** 92)     # grows past 1e30 after a few iterations
+    y[6, ::3] = -0.0                  # signed zeros: canonicalised, never a premise break
+    y[7] = np.where(np.arange(N) % 2 == 0, 0.5, -1.0)   # ties in every row
+    y[9] = y[8]                       # the pair partner of an unbroken frame is decoded alike
+    A = O.Alist(code_path(code))
+    for T in (1, 7, 30):
+        cfg = native.DecoderConfig(T=T, precision=native.F32, **v)
+        assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
+        d, fr, cnt = ctx.decode(y, cfg)
+        redo = ctx.redo_count()
+        want = A.decode(y, T, O.Cfg(**v), workers=8)
+        mism = (d != want).sum(axis=1)
+        assert int(mism.sum()) == 0, f"T={T}: mismatching frames {np.nonzero(mism)[0].tolist()}"
+        w = (want != 1).sum(axis=1)
+        assert np.array_equal(fr["bit_err"], w)
+        assert cnt.frames == len(y) and cnt.bit_err == int(w.sum()) and cnt.iters == T * len(y)
+        # pairs (0,1), (2,3), (4,5) break (frame 5 shares frame 4's pair); a pair is re-decoded whole
+        assert redo == 6, redo
+        monkeypatch.delenv("LDPC_ROWS32")
+        assert ctx.kernel_info(cfg)["kernel"] == "rows"
+        d_old, fr_old, cnt_old = ctx.decode(y, cfg)
+        monkeypatch.setenv("LDPC_ROWS32", "fast")
+        assert np.array_equal(d_old, d) and np.array_equal(fr_old, fr) and cnt_old.bit_err == cnt.bit_err
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ebn0", [1.5, 1.75])
 @pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0))])
 def test_f64_headline_config_bit_exact(gpu_ctx_factory, ebn0, vname, v):
@@ -136,15 +189,21 @@ def test_f64_headline_config_bit_exact(gpu_ctx_factory, ebn0, vname, v):
 @pytest.mark.gpu
 @pytest.mark.parametrize("ebn0", [1.5, 1.75])
 @pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0))])
-def test_f32_bench_kernel_bit_exact_at_T50(gpu_ctx_factory, ebn0, vname, v):
-    """The fp32 row kernel (k_decode_rows<float, PHILOX, 2, 8, 4, 2>: fast check node,
+def test_f32_bench_kernel_bit_exact_at_T50(gpu_ctx_factory, monkeypatch, ebn0, vname, v):
+    """The fp32 bench kernel (k_decode_rows<float, PHILOX, 2, 8, 4, 2>: fast check node,
     reciprocal NMS, fast->exact hand-over) at the bench's T=50 on 2048 codewords per
-    point: decisions identical to the fp32 oracle on the same y."""
+    point: decisions identical to the fp32 oracle on the same y, and
+    to the opt-in pair instance of rows_fast (LDPC_ROWS32=fast)."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory("80211n_1944_r12.alist")
     cfg = native.DecoderConfig(T=50, precision=native.F32, **v)
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
     y, d, fr, cnt = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261017, stream_id=2, first_cw=0, batch=2048)
+    monkeypatch.setenv("LDPC_ROWS32", "fast")
+    y_f, d_f, fr_f, _ = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261017, stream_id=2, first_cw=0, batch=2048)
+    assert ctx.redo_count() == 0
+    monkeypatch.delenv("LDPC_ROWS32")
+    assert np.array_equal(y_f, y) and np.array_equal(d_f, d) and np.array_equal(fr_f, fr)
     want = O.Alist(code_path("80211n_1944_r12.alist")).decode(y, 50, O.Cfg(**v), workers=16)
     assert int((d != want).sum()) == 0
     assert np.array_equal(fr["bit_err"], (want != 1).sum(axis=1))
