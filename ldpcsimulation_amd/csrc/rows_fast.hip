@@ -218,7 +218,10 @@ __device__ __forceinline__ void lds_put(uint32_t addr, const P &v)
 }
 
 template <int RPT> struct FastShape;
-template <> struct FastShape<1> { static constexpr int threads = 1024, waves_per_eu = 4; };
+#ifndef LDPC_FAST_RPT1_WAVES
+#define LDPC_FAST_RPT1_WAVES 4
+#endif
+template <> struct FastShape<1> { static constexpr int threads = 1024, waves_per_eu = LDPC_FAST_RPT1_WAVES; };
 template <> struct FastShape<2> { static constexpr int threads = 512, waves_per_eu = 4; };
 
 template <typename F, int SRC, int C, int DC, int CPT, int RPT, int VAR, bool FDIV>

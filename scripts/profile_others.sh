@@ -17,4 +17,6 @@ run bp_f32 codes/80211n_1944_r12.alist --batch 16384 --T 50 --snr 1.5 --variant 
 run ngdbf codes/80211n_1944_r12.alist --batch 65536 --T 100 --snr 3.5 --decoder gdbf --reps 2
 run dvbs2_flood "$DVB" --batch 2048 --T 50 --snr 1.0 --variant nms --reps 2
 run dvbs2_layered "$DVB" --batch 2048 --T 50 --snr 1.0 --variant nms --schedule layered --reps 2
+run dvbs2_layered_f64 "$DVB" --batch 2048 --T 50 --snr 1.0 --variant nms --schedule layered --reps 2 --prec f64
+run dvbs2_flood_f64 "$DVB" --batch 2048 --T 50 --snr 1.0 --variant nms --reps 2 --prec f64
 echo done
