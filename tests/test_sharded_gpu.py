@@ -9,7 +9,11 @@ all-reduce, so sharing the card changes nothing but speed), decode config 2
 1.5 dB to the reference's stop rule. Their totals and error-weight
 histogram must equal one rank's, for a different batch size too: the frames
 are keyed by global index, and the exact-stop cut makes the result a
-frame-by-frame run of the same noise."""
+frame-by-frame run of the same noise.
+
+Config 3's sweep (sweep.py --schedule layered: DVB-S2 N=64800, layered NMS,
+the global layered kernel) is run the same way, two ranks against one, at one
+SNR point of the sweep."""
 import os
 import socket
 
@@ -20,21 +24,27 @@ from conftest import code_path
 
 CODE = "80211n_1944_r12.alist"
 EBN0, SEED, T = 1.5, 20261018, 50
+# config 3: DVB-S2 layered, one point of the SNR sweep (fp32, the sweep's default precision)
+DVB_CODE, DVB_EBN0, DVB_T = "dvbs2_1_2.alist", 1.0, 10
 
 
-def _cfg():
+def _cfg(case="c2"):
     from ldpcsimulation_amd import native
+    if case == "c3":
+        return native.DecoderConfig(variant=native.NMS, alpha=1.25, T=DVB_T, precision=native.F32,
+                                    schedule=native.LAYERED)
     return native.DecoderConfig(variant=native.NMS, alpha=1.25, T=T, precision=native.F64)
 
 
-def _run(ctx, batch):
+def _run(ctx, batch, case="c2"):
     from ldpcsimulation_amd import sim
-    cfg = _cfg()
+    cfg = _cfg(case)
+    ebn0, t = (DVB_EBN0, DVB_T) if case == "c3" else (EBN0, T)
 
     def run_batch(first, n):
-        fr, _ = ctx.sim_batch(EBN0, 0.5, cfg, SEED, 0, first, n)
+        fr, _ = ctx.sim_batch(ebn0, 0.5, cfg, SEED, 0, first, n)
         return fr
-    return sim.simulate_point(run_batch, ctx.graph.N, T, EBN0, batch, device=0)
+    return sim.simulate_point(run_batch, ctx.graph.N, t, ebn0, batch, device=0)
 
 
 def _run_async(ctx, batch):
@@ -56,14 +66,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, batch, path, q):
+def _worker(rank, world, port, batch, path, q, case="c2"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from ldpcsimulation_amd import native
         ctx = native.Context(native.Graph.from_alist(path), 0, batch)
-        res = _run(ctx, batch)
+        res = _run(ctx, batch, case)
         q.put((rank, res.counts, res.hist.tolist(), res.rounds))
     except Exception as e:   # report, never hang the parent
         q.put((rank, repr(e), None, None))
@@ -87,6 +97,31 @@ def test_two_ranks_on_the_hip_path_equal_one_rank(gpu_ctx_factory):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, 1024, code_path(CODE), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, counts, hist, rounds in out:
+        assert isinstance(counts, dict), counts
+        assert counts == one.counts, (rank, counts, one.counts)
+        assert np.array_equal(np.array(hist), one.hist), rank
+
+
+@pytest.mark.gpu
+def test_dvbs2_layered_sweep_point_two_ranks_equal_one_rank(gpu_ctx_factory):
+    """Config 3 on the HIP path: one SNR point of the DVB-S2 layered sweep, two gloo
+    ranks (batch 48 each) against one rank at batch 96 and at batch 40."""
+    import torch.multiprocessing as mp
+    one = _run(gpu_ctx_factory(DVB_CODE, 96), 96, "c3")
+    assert one.counts["frame_err"] >= 40 and one.counts["bit_err"] >= 200
+    other = _run(gpu_ctx_factory(DVB_CODE, 40), 40, "c3")
+    assert other.counts == one.counts and np.array_equal(other.hist, one.hist)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 48, code_path(DVB_CODE), q, "c3")) for r in range(2)]
     for p in procs:
         p.start()
     out = [q.get(timeout=240) for _ in procs]
