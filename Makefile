@@ -98,6 +98,13 @@ fastvariant: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/rows_fast.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/rows_fast.o
 
+# GDBF kernel A/B variants: make gdbfvariant NAME=x VFLAGS="-DLDPC_GDBF_..." -> lib/variants/libldpc_hip_x.so
+gdbfvariant: $(OBJS)
+	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/gdbf.o $(CSRC)/gdbf.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/gdbf.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/gdbf.o
+
 oracle:
 	$(MAKE) -f oracle/Makefile
 

@@ -981,14 +981,14 @@ static void gdbf_fill(ldpc::GdbfArgs &a, ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, 
 
 static int gdbf_run(ldpc_ctx *c, const ldpc::GdbfArgs &a, bool f64)
 {
-    const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, f64);
+    const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, f64, a.flags, c->g->maxdv, c->g->maxdc);
     int slots = 0;
     if (ch.slot_bytes) {
         slots = std::min(a.batch, 2 * c->num_cus);
         HIP_TRY(c->gscratch.ensure(ch.slot_bytes * (size_t)slots));
     }
     HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    HIP_TRY(ldpc::gdbf_launch(c->dg, a, f64, ch, c->gscratch.p, slots, c->stream));
+    HIP_TRY(ldpc::gdbf_launch(c->dg, a, f64, ch, c->gscratch.p, slots, c->num_cus, c->stream));
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     return LDPC_OK;
@@ -1145,7 +1145,7 @@ int ldpc_gdbf_kernel_info(ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, char *name, int
     int rc = gdbf_check_cfg(cfg);
     if (rc) return rc;
     if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
-    const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, cfg->precision == LDPC_F64);
+    const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, cfg->precision == LDPC_F64, cfg->flags, c->g->maxdv, c->g->maxdc);
     if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", ch.name);
     if (lds_bytes) *lds_bytes = ch.lds_bytes;
     return LDPC_OK;

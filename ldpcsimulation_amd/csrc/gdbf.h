@@ -29,14 +29,19 @@ struct GdbfArgs {
 };
 
 struct GdbfChoice {
-    const char *name = "";          // "gdbf_lds" | "gdbf_global"
+    const char *name = "";          // "gdbf_rows" | "gdbf_lds" | "gdbf_global"
     int lds_bytes = 0, threads = 0;
     size_t slot_bytes = 0;          // global kernel: state bytes per resident codeword
+    int dvm = 0;                    // gdbf_rows: bit-degree bound of the register schedule (4 or 12)
 };
 
-GdbfChoice gdbf_choose(const DevGraph &g, bool f64);
-// scratch: slots * choice.slot_bytes bytes for the global kernel (persistent grid of `slots`).
+// flags: the decoder's GDBF_* switches; maxdv / maxdc: the code's largest
+// column / row degree. LDPC_GDBF_KERNEL=generic in the environment forces the
+// one-workgroup-per-codeword kernels (tests compare the two).
+GdbfChoice gdbf_choose(const DevGraph &g, bool f64, int flags, int maxdv, int maxdc);
+// scratch: slots * choice.slot_bytes bytes for the global kernel (persistent grid of `slots`);
+// num_cus sizes the persistent grid of gdbf_rows.
 hipError_t gdbf_launch(const DevGraph &g, const GdbfArgs &a, bool f64, const GdbfChoice &ch, void *scratch,
-                       int slots, hipStream_t s);
+                       int slots, int num_cus, hipStream_t s);
 
 }  // namespace ldpc

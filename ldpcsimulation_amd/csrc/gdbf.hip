@@ -27,6 +27,8 @@
 #include "minsum_common.h"
 
 #include <hip/hip_runtime.h>
+#include <cstdlib>
+#include <cstring>
 
 namespace ldpc {
 
@@ -90,6 +92,24 @@ __device__ __forceinline__ F gdbf_objective(const DevGraph &g, const int8_t *d, 
     for (int i = 0; i < g.N; ++i) f += (F)d[i] * yq[i];
     for (int j = 0; j < g.M; ++j) f += (F)s[j];
     return f;
+}
+
+// NGDBF perturbation normals (the noise of :318-333, which the reference draws
+// from glibc random() by Box-Muller, rand.h:19-20): Box-Muller on the hardware
+// transcendentals -- v_log_f32 (log2), v_sqrt_f32, v_sin_f32 / v_cos_f32 (which
+// take revolutions, so 2*pi*a needs no multiply) -- instead of OCML's correctly
+// rounded logf / sqrtf / sincospif: a few ulp of error in a random perturbation
+// leaves its distribution unchanged, and it is ~10x fewer instructions (the
+// accurate form was ~80 % of the parallel-flip iteration). Both GDBF kernels use
+// it, so they decode identical perturbations; parity with the reference's own
+// perturbation draws goes through the caller-given path (SRC_GIVEN).
+__device__ __forceinline__ void pert_normals(uint32_t ua, uint32_t ur, float &n0, float &n1)
+{
+    const float a = (float)ua * 2.3283064365386963e-10f + 1.1641532182693481e-10f;   // (0, 1]
+    const float r = (float)ur * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
+    const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(r));   // sqrt(-2 ln r)
+    n0 = rad * __builtin_amdgcn_cosf(a);
+    n1 = rad * __builtin_amdgcn_sinf(a);
 }
 
 template <typename F, int SRC>
@@ -188,11 +208,11 @@ __device__ __forceinline__ void gdbf_codeword(const GdbfArgs &a, const DevGraph 
 #pragma unroll
                         for (int q = 0; q < 4; ++q) pv[q] = ((F)u[q] + F(0.5)) * (F)0x1p-32;   // in (0, 1)
                     } else {
-                        F n[4];
-                        box_muller(u[0], u[1], n[0], n[1]);
-                        box_muller(u[2], u[3], n[2], n[3]);
+                        float n[4];
+                        pert_normals(u[0], u[1], n[0], n[1]);
+                        pert_normals(u[2], u[3], n[2], n[3]);
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) pv[q] = nsig * n[q];
+                        for (int q = 0; q < 4; ++q) pv[q] = nsig * (F)n[q];
                     }
                 }
             }
@@ -335,11 +355,326 @@ __global__ __launch_bounds__(1024) void k_gdbf_global(GdbfArgs a, DevGraph g, Gd
                               reinterpret_cast<int8_t *>(base + L.s), red, redE, redI, fobj);
 }
 
-constexpr size_t kGdbfMaxLds = 64 * 1024;
+// ---------------------------------------------------------------------
+// gdbf_rows: the parallel-flip family (MNGDBF, SMNGDBF, ATGDBF, SATGDBF, SMGDBF
+// and their quantised / saturated forms; no SEQUENTIAL, MODESWITCH or QPROB)
+// for codes with N <= 4 * 1024, row degree <= 8 and column degree <= 12 --
+// config 4 (802.11n N=1944). Same arithmetic, in the same order, as
+// gdbf_codeword; what differs is where the state lives:
+//  * thread t owns the Philox group of bits 4t..4t+3 (the counter the channel
+//    and the perturbations are keyed by) and rows t and t + blockDim;
+//  * the Tanner graph sits in registers, loaded once per workgroup: a row's 8
+//    bit indices and a bit's <= DVM check indices in nlist order, 16 bits each;
+//    padding entries point at a dummy bit (d = +1) or a dummy check whose
+//    term is -0.0 (E + -0.0 == E for every E, so E is exactly the reference's sum);
+//  * yq, theta, dsum and d of the thread's bits stay in registers; LDS holds
+//    the d < 0 flags as bytes (one 32-bit word per thread; a row's parity is
+//    the xor of its bytes) and, per check, the term w * s_j in F (the check
+//    thread computes the product a bit would, so a bit adds one LDS word per
+//    edge), plus a double-buffered early-stop flag, so the early stop costs one
+//    barrier instead of __syncthreads_or's reduction;
+//  * a bit slot's syndrome reads are issued together, up to the wave's largest
+//    degree (a uniform bound), not the code's; the row gathers are issued
+//    before the perturbations are generated; the workgroup is persistent.
+// ---------------------------------------------------------------------
+struct GdbfRowsLayout {
+    int np, soff, floff, total;
+};
+static GdbfRowsLayout gdbf_rows_layout(int N, int M, int fsz)
+{
+    GdbfRowsLayout L;
+    L.np = ((N + 3) & ~3) + 4;                // d < 0 flags [0..N) + pad; the last word: dummy bits (0)
+    L.soff = (L.np + 7) & ~7;
+    L.floff = L.soff + ((M + 1) * fsz + 7) / 8 * 8;   // w*s[0..M) as F, [M] = the dummy check (-0.0)
+    L.total = L.floff + 16;                   // flags[2] (+ pad)
+    return L;
+}
 
-GdbfChoice gdbf_choose(const DevGraph &g, bool f64)
+// NT = 512 (N <= 2048) or 1024 threads, at most 128 VGPRs (4 waves/SIMD: two
+// 512-thread workgroups per CU). Measured (config 4, fp32): more waves bought
+// with fewer registers spill in the iteration loop (5 / 6 waves/SIMD: 48 / 54 ms
+// against 36 ms), and 2 bits per thread in 1024-thread workgroups (each pair of
+// lanes running the same Philox call) took 48 ms -- the Philox multiplies are a
+// large share of the iteration, and a codeword's iteration is a chain of LDS
+// round trips and barriers that more waves per codeword do not shorten.
+template <typename F, int SRC, int DVM, int NT>
+__global__ __launch_bounds__(NT, 1024 / NT * 2) void k_gdbf_rows(GdbfArgs a, DevGraph g, int np, int soff, int floff)
+{
+    constexpr int DC = 8, BPT = 4, RPT = 2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int red[16 * 4];
+    uint8_t *dl = smem;                                // 1 where d = -1
+    F *sl = reinterpret_cast<F *>(smem + soff);        // w * s_j, the term a bit adds for check j
+    volatile int *fl = reinterpret_cast<int *>(smem + floff);
+    const int tid = threadIdx.x;
+    const int N = g.N, M = g.M, T = a.T;
+    const int dbit = np - 1;              // dummy bit index
+    const int v0 = BPT * tid;             // the thread's first bit
+    const int g4 = tid;                   // its Philox group
+    // ---- the graph, into registers (once per workgroup) ----
+    uint32_t rc[RPT][DC / 2];
+    bool rvalid[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+        const int j = tid + r * NT;
+        rvalid[r] = j < M;
+        const int deg = rvalid[r] ? g.row_deg[j] : 0;
+#pragma unroll
+        for (int k = 0; k < DC; k += 2) {
+            const uint32_t c0 = k < deg ? (uint32_t)g.row_cols[(size_t)j * g.dcs + k] : (uint32_t)dbit;
+            const uint32_t c1 = k + 1 < deg ? (uint32_t)g.row_cols[(size_t)j * g.dcs + k + 1] : (uint32_t)dbit;
+            rc[r][k / 2] = c0 | (c1 << 16);
+        }
+    }
+    const bool own = v0 < N;
+    uint32_t bc[BPT][DVM / 2];
+    int wdeg[BPT];   // wave-uniform bound of each slot's degree
+#pragma unroll
+    for (int q = 0; q < BPT; ++q) {
+        const int i = v0 + q;
+        int e0 = 0, deg = 0;
+        if (i < N) {
+            e0 = g.col_ptr[i];
+            deg = g.col_ptr[i + 1] - e0;
+        }
+#pragma unroll
+        for (int k = 0; k < DVM; k += 2) {
+            const uint32_t j0 = k < deg ? g.col_refs[e0 + k] >> 6 : (uint32_t)M;
+            const uint32_t j1 = k + 1 < deg ? g.col_refs[e0 + k + 1] >> 6 : (uint32_t)M;
+            bc[q][k / 2] = j0 | (j1 << 16);
+        }
+        int m = deg;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        wdeg[q] = __builtin_amdgcn_readfirstlane(m);
+    }
+    if (tid == 0) {
+        *reinterpret_cast<uint32_t *>(dl + np - 4) = 0u;   // dummy bits: d = +1
+        sl[M] = -F(0);                                      // dummy check: E + -0.0 == E for every E
+    }
+    const bool smooth = (a.flags & GDBF_SMOOTH) != 0, noise = (a.flags & GDBF_NOISE) != 0;
+    const bool adapt = (a.flags & GDBF_ADAPT) != 0;
+    const F w = (F)a.w, lambda = (F)a.lambda, nsig = (F)a.noise_sigma;
+    const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+
+    for (int b = blockIdx.x; b < a.batch; b += gridDim.x) {
+        const uint64_t cw = a.first_cw + (uint64_t)b;
+        const int8_t *cvec = nullptr;
+        if (SRC == SRC_GIVEN) {
+            if (a.c) cvec = a.c + (size_t)b * N;
+        } else if (a.cw_table) {
+            cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
+        }
+        // ---- channel + front-end (:251-274), as gdbf_codeword ----
+        F yq[BPT], theta[BPT];
+        int d[BPT], dsum[BPT];
+        int unc = 0;
+#pragma unroll
+        for (int q = 0; q < BPT; ++q) {
+            yq[q] = F(0);
+            theta[q] = (F)a.theta0;
+            d[q] = 1;
+            dsum[q] = 0;
+        }
+        if (own) {
+            F yv[BPT];
+            if (SRC == SRC_GIVEN) {
+                const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
+#pragma unroll
+                for (int q = 0; q < BPT; ++q) yv[q] = (v0 + q < N) ? y[v0 + q] : F(1);
+            } else {
+                uint32_t u[4];
+                philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                F n[4];
+                box_muller(u[0], u[1], n[0], n[1]);
+                box_muller(u[2], u[3], n[2], n[3]);
+                const F sigma = (F)a.sigma;
+#pragma unroll
+                for (int q = 0; q < BPT; ++q) {
+                    const int v = v0 + q;
+                    yv[q] = (F)(v < N && cvec ? cvec[v] : 1) * (F(1) + sigma * n[q]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const int v = v0 + q;
+                if (v < N) {
+                    int r;
+                    yq[q] = gdbf_front<F>(yv[q], a, r);
+                    const int cv = cvec ? cvec[v] : 1;
+                    unc += (r * cv < 0);
+                    d[q] = r;
+                }
+            }
+        }
+        auto put_d = [&]() {
+            if (own)
+                *reinterpret_cast<uint32_t *>(dl + v0) = (uint32_t)(d[0] < 0) | ((uint32_t)(d[1] < 0) << 8) |
+                                                         ((uint32_t)(d[2] < 0) << 16) | ((uint32_t)(d[3] < 0) << 24);
+        };
+        put_d();
+        if (tid == 0) {
+            fl[0] = 0;
+            fl[1] = 0;
+        }
+        __syncthreads();
+
+        int it;
+        bool sat = false;
+        for (it = 0; it < T; ++it) {
+            // the packed 16-bit schedule words are opaque per iteration: otherwise the
+            // compiler hoists the unpacked indices out of the loop and spills them
+#pragma unroll
+            for (int r = 0; r < RPT; ++r)
+#pragma unroll
+                for (int k = 0; k < DC / 2; ++k) asm volatile("" : "+v"(rc[r][k]));
+#pragma unroll
+            for (int q = 0; q < BPT; ++q)
+#pragma unroll
+                for (int k = 0; k < DVM / 2; ++k) asm volatile("" : "+v"(bc[q][k]));
+            // ---- check nodes (:517-534); the row gathers are issued first and their
+            // LDS latency is covered by this iteration's perturbations (which do not
+            // depend on the decoder state; one spare set on the iteration that stops) ----
+            uint32_t g8[RPT][DC];
+#pragma unroll
+            for (int r = 0; r < RPT; ++r)
+#pragma unroll
+                for (int k = 0; k < DC; ++k) g8[r][k] = dl[(rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu];
+            F pv[BPT];
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) pv[q] = F(0);
+            if (noise && own) {
+                if (SRC == SRC_GIVEN) {
+                    const F *pr = reinterpret_cast<const F *>(a.pert) + ((size_t)b * T + it) * N;
+#pragma unroll
+                    for (int q = 0; q < BPT; ++q) pv[q] = (v0 + q < N) ? pr[v0 + q] : F(0);
+                } else {
+                    uint32_t u[4];
+                    philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32),
+                                  (a.stream_id & 0xFFFFFu) | ((uint32_t)(it + 1) << 20), k0, k1, u);
+                    float n[4];
+                    pert_normals(u[0], u[1], n[0], n[1]);
+                    pert_normals(u[2], u[3], n[2], n[3]);
+#pragma unroll
+                    for (int q = 0; q < BPT; ++q) pv[q] = nsig * (F)n[q];
+                }
+            }
+            int fail = 0;
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) {
+                uint32_t p = 0;
+#pragma unroll
+                for (int k = 0; k < DC; ++k) p ^= g8[r][k];
+                if (rvalid[r]) sl[tid + r * NT] = w * (p ? F(-1) : F(1));   // w * (F)s_j, as :541-551 adds it
+                fail |= (int)p;
+            }
+            if (fail) fl[it & 1] = 1;
+            __syncthreads();
+            sat = fl[it & 1] == 0;   // :305-306, uniform over the workgroup
+            if (sat) break;
+            if (tid == 0) fl[(it + 1) & 1] = 0;   // nobody reads or sets it before the next barrier
+            // ---- bit nodes (:536-621), mu = 1 ----
+            const bool acc_smooth = smooth && it > T - a.windowsize;   // :349
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                // all of the slot's syndrome reads first (one LDS round trip, not one per
+                // edge: a read inside the guarded add could not be issued before the
+                // previous add), up to the wave's largest degree; the adds keep the
+                // reference's order and skip this lane's padding by a select
+                // :541-551 in nlist order, padding adds -0.0: the first K0 terms (every
+                // slot reads them), then, behind one uniform branch, the rest
+                constexpr int K0 = DVM < 4 ? DVM : 4;
+                F sv[K0];
+#pragma unroll
+                for (int k = 0; k < K0; ++k) sv[k] = sl[(bc[q][k / 2] >> (16 * (k & 1))) & 0xffffu];
+                F E = (F)d[q] * yq[q];
+#pragma unroll
+                for (int k = 0; k < K0; ++k) E += sv[k];
+                if (DVM > K0 && wdeg[q] > K0) {
+                    F sw[DVM - K0 > 0 ? DVM - K0 : 1];
+#pragma unroll
+                    for (int k = K0; k < DVM; ++k) sw[k - K0] = sl[(bc[q][k / 2] >> (16 * (k & 1))) & 0xffffu];
+#pragma unroll
+                    for (int k = K0; k < DVM; ++k)
+                        if (k < wdeg[q]) E += sw[k - K0];
+                }
+                if (noise) E += pv[q];
+                const bool flip = E < theta[q];             // :598-603
+                const int dn = flip ? -d[q] : d[q];
+                if (adapt && !flip) theta[q] *= lambda;     // :612-617
+                if (acc_smooth) dsum[q] += dn;              // :348-354
+                d[q] = dn;
+            }
+#pragma unroll
+            for (int q = 0; q < BPT; ++q)   // bits past N keep +1
+                if (v0 + q >= N) d[q] = 1;
+            put_d();
+            __syncthreads();
+        }
+        if (smooth && !sat) {   // :358-367
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) d[q] = (v0 + q < N) ? (dsum[q] > 0 ? 1 : -1) : 1;
+            put_d();
+        }
+        __syncthreads();
+
+        // ---- error weight (:378), syndrome of the output, accounting ----
+        int wgt = 0, synd = 0;
+        if (own)
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                const int v = v0 + q;
+                if (v < N) {
+                    const int cv = cvec ? cvec[v] : 1;
+                    wgt += (d[q] != cv);
+                    if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d[q];
+                }
+            }
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            uint32_t p = 0;
+#pragma unroll
+            for (int k = 0; k < DC; ++k) p ^= dl[(rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu];
+            synd |= (int)p;
+        }
+        int sums[3] = {wgt, unc, synd};
+        block_sum_n<3>(sums, red);
+        if (tid == 0) {
+            const int sf = sums[2] > 0;
+            atomicAdd(&a.counts[0], (unsigned long long)sums[0]);
+            atomicAdd(&a.counts[1], (unsigned long long)(sums[0] > 0));
+            atomicAdd(&a.counts[2], (unsigned long long)sums[1]);
+            atomicAdd(&a.counts[3], 1ull);
+            atomicAdd(&a.counts[4], (unsigned long long)it);   // totalIterations += it (:399)
+            atomicAdd(&a.counts[5], (unsigned long long)sf);
+            if (sums[0] > 0 && a.hist) atomicAdd(&a.hist[sums[0] - 1], 1ull);
+            if (a.frame_res) a.frame_res[b] = make_int4(sums[0], sums[1], sf, it);
+        }
+        __syncthreads();
+    }
+}
+
+constexpr size_t kGdbfMaxLds = 64 * 1024;
+constexpr int kGdbfRowsUnsupported = GDBF_SEQUENTIAL | GDBF_MODESWITCH | GDBF_QPROB;
+
+static bool gdbf_rows_forced_off()
+{
+    const char *e = std::getenv("LDPC_GDBF_KERNEL");
+    return e && std::strcmp(e, "generic") == 0;
+}
+
+GdbfChoice gdbf_choose(const DevGraph &g, bool f64, int flags, int maxdv, int maxdc)
 {
     GdbfChoice ch;
+    if (!(flags & kGdbfRowsUnsupported) && g.N >= 1 && g.N <= 4 * 1024 && g.M <= 2 * 1024 && maxdc <= 8 &&
+        maxdv <= 12 && !gdbf_rows_forced_off()) {
+        ch.name = "gdbf_rows";
+        ch.threads = g.N <= 4 * 512 && g.M <= 2 * 512 ? 512 : 1024;
+        ch.dvm = maxdv <= 4 ? 4 : 12;
+        ch.lds_bytes = gdbf_rows_layout(g.N, g.M, f64 ? 8 : 4).total;
+        ch.slot_bytes = 0;
+        return ch;
+    }
     const GdbfLayout L = gdbf_layout(g.N, g.M, f64 ? 8 : 4);
     if (L.total <= kGdbfMaxLds) {
         ch.name = "gdbf_lds";
@@ -355,10 +690,33 @@ GdbfChoice gdbf_choose(const DevGraph &g, bool f64)
     return ch;
 }
 
+template <typename F, int SRC, int DVM, int NT>
+static hipError_t gdbf_rows_launch_b(const DevGraph &g, const GdbfArgs &a, int num_cus, hipStream_t s)
+{
+    const GdbfRowsLayout L = gdbf_rows_layout(g.N, g.M, (int)sizeof(F));
+    auto fn = k_gdbf_rows<F, SRC, DVM, NT>;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, L.total) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    int grid = per_cu * (num_cus > 0 ? num_cus : 1);
+    if (grid > a.batch) grid = a.batch;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(NT), L.total, s, a, g, L.np, L.soff, L.floff);
+    return hipGetLastError();
+}
+template <typename F, int SRC, int DVM>
+static hipError_t gdbf_rows_launch(const DevGraph &g, const GdbfArgs &a, const GdbfChoice &ch, int num_cus,
+                                   hipStream_t s)
+{
+    return ch.threads == 512 ? gdbf_rows_launch_b<F, SRC, DVM, 512>(g, a, num_cus, s)
+                             : gdbf_rows_launch_b<F, SRC, DVM, 1024>(g, a, num_cus, s);
+}
+
 template <typename F, int SRC>
 static hipError_t gdbf_launch_t(const DevGraph &g, const GdbfArgs &a, const GdbfChoice &ch, void *scratch,
-                                int slots, hipStream_t s)
+                                int slots, int num_cus, hipStream_t s)
 {
+    if (ch.dvm == 4) return gdbf_rows_launch<F, SRC, 4>(g, a, ch, num_cus, s);
+    if (ch.dvm == 12) return gdbf_rows_launch<F, SRC, 12>(g, a, ch, num_cus, s);
     const GdbfLayout L = gdbf_layout(g.N, g.M, sizeof(F));
     if (ch.lds_bytes > 0) {
         hipLaunchKernelGGL((k_gdbf_lds<F, SRC>), dim3(a.batch), dim3(ch.threads), ch.lds_bytes, s, a, g, L);
@@ -372,14 +730,14 @@ static hipError_t gdbf_launch_t(const DevGraph &g, const GdbfArgs &a, const Gdbf
 }
 
 hipError_t gdbf_launch(const DevGraph &g, const GdbfArgs &a, bool f64, const GdbfChoice &ch, void *scratch,
-                       int slots, hipStream_t s)
+                       int slots, int num_cus, hipStream_t s)
 {
     if (a.batch <= 0) return hipSuccess;
     if (f64)
-        return a.src == SRC_GIVEN ? gdbf_launch_t<double, SRC_GIVEN>(g, a, ch, scratch, slots, s)
-                                  : gdbf_launch_t<double, SRC_PHILOX>(g, a, ch, scratch, slots, s);
-    return a.src == SRC_GIVEN ? gdbf_launch_t<float, SRC_GIVEN>(g, a, ch, scratch, slots, s)
-                              : gdbf_launch_t<float, SRC_PHILOX>(g, a, ch, scratch, slots, s);
+        return a.src == SRC_GIVEN ? gdbf_launch_t<double, SRC_GIVEN>(g, a, ch, scratch, slots, num_cus, s)
+                                  : gdbf_launch_t<double, SRC_PHILOX>(g, a, ch, scratch, slots, num_cus, s);
+    return a.src == SRC_GIVEN ? gdbf_launch_t<float, SRC_GIVEN>(g, a, ch, scratch, slots, num_cus, s)
+                              : gdbf_launch_t<float, SRC_PHILOX>(g, a, ch, scratch, slots, num_cus, s);
 }
 
 }  // namespace ldpc

@@ -212,6 +212,32 @@ def test_gdbf_sim_independent_of_batch_split(gpu_ctx_factory):
     assert np.array_equal(full, np.concatenate([a, b]))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("code", ["80211n_1944_r12.alist", "PEGReg504x1008.alist", "4000.2000.4.244.alist"])
+@pytest.mark.parametrize("vname", ["SMNGDBF", "MNGDBF", "ATGDBF", "SATGDBF", "QSMNGDBF"])
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_gdbf_rows_kernel_equals_generic_kernel(gpu_ctx_factory, monkeypatch, code, vname, prec):
+    """The register-schedule kernel (gdbf_rows) and the one-workgroup-per-codeword kernel
+    decode the same on-device Philox channel and perturbations to identical per-frame
+    results (error weight, uncoded errors, syndrome, iterations) and counters."""
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(code, 2048)
+    c = dict(COMMON, **GPU_VARIANTS[vname])
+    cfg = _gpu_cfg(native, c, prec == "f32")
+    assert ctx.gdbf_kernel_info(cfg)["kernel"] == "gdbf_rows"
+    res = {}
+    for snr in (2.0, 3.0):
+        fr, cnt = ctx.gdbf_sim_batch(snr, 0.5, cfg, seed=31, stream_id=2, first_cw=100, batch=2048)
+        res[snr] = (fr, cnt.as_dict())
+    monkeypatch.setenv("LDPC_GDBF_KERNEL", "generic")
+    assert ctx.gdbf_kernel_info(cfg)["kernel"] != "gdbf_rows"
+    for snr in (2.0, 3.0):
+        fr, cnt = ctx.gdbf_sim_batch(snr, 0.5, cfg, seed=31, stream_id=2, first_cw=100, batch=2048)
+        assert np.array_equal(fr, res[snr][0]), (snr, int((fr != res[snr][0]).sum()))
+        assert cnt.as_dict() == res[snr][1]
+    assert res[2.0][1]["frame_err"] > 0   # the comparison covers failing frames too
+
+
 def test_unsupported_flag_combinations_are_rejected():
     """ADAPT with single-bit flips and NOISE with QPROB have no reference target; the
     ABI refuses them instead of guessing (checked before any device call)."""
