@@ -8,17 +8,30 @@ namespace ldpc {
 
 // ---------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. SC'11) + Box-Muller: 4 normals per call.
+// LDPC_PHILOX_MAD64: the two 32x32->64 products of a round as v_mad_u64_u32
+// (same values either way). On in gdbf.hip, where Philox runs every iteration;
+// off elsewhere: in the fp64 row kernel, which draws once per codeword, the
+// 64-bit form costs 2.5 % through register allocation (16.10 vs 16.52 ms,
+// 3 interleaved rounds).
 // ---------------------------------------------------------------------
+#ifndef LDPC_PHILOX_MAD64
+#define LDPC_PHILOX_MAD64 0
+#endif
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1, uint32_t out[4])
 {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
+#if LDPC_PHILOX_MAD64
         // one v_mad_u64_u32 per product (lo and hi together) instead of a
         // v_mul_lo_u32 + v_mul_hi_u32 pair: 20 quarter-rate multiplies per call, not 40
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
         const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
         const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
+#else
+        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+#endif
         const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;

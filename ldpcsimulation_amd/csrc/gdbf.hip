@@ -22,6 +22,7 @@
 // verification, given by the caller as pert[frame][it][bit].
 // Compiled with -ffp-contract=off: E is accumulated with the reference's
 // operation order, so fp64 decisions equal the reference's for the same noise.
+#define LDPC_PHILOX_MAD64 1   // Philox every iteration: 20 instead of 40 quarter-rate multiplies
 #include "gdbf.h"
 #include "device_common.h"
 #include "minsum_common.h"
@@ -390,15 +391,22 @@ static GdbfRowsLayout gdbf_rows_layout(int N, int M, int fsz)
     return L;
 }
 
-// NT = 512 (N <= 2048) or 1024 threads, at most 128 VGPRs (4 waves/SIMD: two
-// 512-thread workgroups per CU). Measured (config 4, fp32): more waves bought
-// with fewer registers spill in the iteration loop (5 / 6 waves/SIMD: 48 / 54 ms
-// against 36 ms), and 2 bits per thread in 1024-thread workgroups (each pair of
-// lanes running the same Philox call) took 48 ms -- the Philox multiplies are a
-// large share of the iteration, and a codeword's iteration is a chain of LDS
-// round trips and barriers that more waves per codeword do not shorten.
+// NT = 512 (N <= 2048) or 1024 threads. Measured on the way (config 4, fp32):
+// 2 bits per thread in 1024-thread workgroups (each pair of lanes running the
+// same Philox call) was slower (48 vs 36 ms at that stage) -- the kernel is
+// VALU-bound, Philox is a large share of it, and more waves per codeword do
+// not shorten a codeword's chain of LDS round trips and barriers.
+// Waves per SIMD the 512-thread instances are bounded to (fp32 / fp64): 6 = three
+// workgroups per CU at 80 VGPRs, measured 22.8 vs 24.5 ms at 4 (fp32, config 4)
+// despite a few spilled registers.
+#ifndef LDPC_GDBF_ROWS_WAVES
+#define LDPC_GDBF_ROWS_WAVES 6
+#endif
+#ifndef LDPC_GDBF_ROWS_WAVES64
+#define LDPC_GDBF_ROWS_WAVES64 4
+#endif
 template <typename F, int SRC, int DVM, int NT>
-__global__ __launch_bounds__(NT, 1024 / NT * 2) void k_gdbf_rows(GdbfArgs a, DevGraph g, int np, int soff, int floff)
+__global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS_WAVES : LDPC_GDBF_ROWS_WAVES64) void k_gdbf_rows(GdbfArgs a, DevGraph g, int np, int soff, int floff)
 {
     constexpr int DC = 8, BPT = 4, RPT = 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
