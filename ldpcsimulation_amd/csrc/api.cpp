@@ -504,7 +504,7 @@ static int nms_setup(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, ldpc::DecodeArgs 
 
 static ldpc::KernelChoice select_kernel(const ldpc_ctx *c, bool f64, int schedule, int variant)
 {
-    if (variant == LDPC_BP) return ldpc::bp_choose(c->dg, f64);
+    if (variant == LDPC_BP) return ldpc::bp_choose(c->dg, f64, c->g->E);
     if (schedule == LDPC_LAYERED)
         return ldpc::choose_layered(c->dg, f64, c->fs, c->ls, c->force[0] ? c->force : nullptr);
     return ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr,
@@ -550,7 +550,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
             HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks + 65536));   // + the phase kernels' counters
         }
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
-        HIP_TRY(ldpc::bp_launch(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream));
+        HIP_TRY(ldpc::bp_launch(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->g->E, c->num_cus, c->stream));
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
         c->timed = true;
         return LDPC_OK;

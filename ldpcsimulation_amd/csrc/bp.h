@@ -6,9 +6,11 @@ namespace ldpc {
 
 constexpr int kBpMaxDc = 32;   // row degree bound of the BP check node (per-thread tanh array)
 
+// "bp_rows" (graph in registers, persistent; N <= 4096, row degree <= 8),
 // "bp_lds" (state in LDS) or "bp_global" (a global slot per resident block).
-KernelChoice bp_choose(const DevGraph &g, bool f64);
+// E: the code's edge count; num_cus sizes bp_rows' persistent grid.
+KernelChoice bp_choose(const DevGraph &g, bool f64, int E);
 hipError_t bp_launch(const DevGraph &g, const DecodeArgs &a, bool f64, const KernelChoice &kc, void *gscratch,
-                     int gblocks, hipStream_t s);
+                     int gblocks, int E, int num_cus, hipStream_t s);
 
 }  // namespace ldpc

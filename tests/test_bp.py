@@ -175,3 +175,28 @@ def test_bp_sim_independent_of_batch_split(gpu_ctx_factory):
     a, _ = ctx.sim_batch(2.0, 0.5, cfg, seed=3, stream_id=0, first_cw=0, batch=120)
     b, _ = ctx.sim_batch(2.0, 0.5, cfg, seed=3, stream_id=0, first_cw=120, batch=180)
     assert np.array_equal(full, np.concatenate([a, b]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("code", CODES)
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_bp_rows_kernel_equals_generic_kernel(gpu_ctx_factory, monkeypatch, code, prec):
+    """The register-schedule BP kernel (bp_rows) and the one-workgroup-per-codeword
+    kernel give identical channel samples, decisions and per-frame results on the
+    on-device Philox path (same arithmetic in the same order)."""
+    native = _native()
+    ctx = gpu_ctx_factory(code, 1024)
+    cfg = native.DecoderConfig(variant=native.BP, T=12, precision=native.F32 if prec == "f32" else native.F64)
+    if code.startswith("4000") and prec == "f64":   # app + messages: 160 KB, beyond one workgroup's LDS
+        assert ctx.kernel_info(cfg)["kernel"] != "bp_rows"
+        return
+    assert ctx.kernel_info(cfg)["kernel"] == "bp_rows"
+    got = [ctx.sim_trace(e, 0.5, cfg, seed=17, stream_id=3, first_cw=64, batch=1024) for e in (1.0, 2.0)]
+    monkeypatch.setenv("LDPC_BP_KERNEL", "generic")
+    assert ctx.kernel_info(cfg)["kernel"] != "bp_rows"
+    for e, (y, d, fr, cnt) in zip((1.0, 2.0), got):
+        y2, d2, fr2, cnt2 = ctx.sim_trace(e, 0.5, cfg, seed=17, stream_id=3, first_cw=64, batch=1024)
+        assert np.array_equal(y, y2) and np.array_equal(fr, fr2), e
+        assert int((d != d2).sum()) == 0, e
+        assert cnt.as_dict() == cnt2.as_dict()
+    assert got[0][3].frame_err > 0   # failing frames are compared too
