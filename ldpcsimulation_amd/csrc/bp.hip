@@ -341,12 +341,18 @@ __global__ __launch_bounds__(NT, NT == 512 ? 4 : 2) void k_bp_rows(DecodeArgs a,
                     if (bp_abs(v) > maxllr) v = maxllr * (v >= F(0) ? F(1) : F(-1));      // :400-401
                     th[k] = k < rdeg[r] ? bp_tanh(v / F(2)) : F(1);
                 }
+                // prod over k != jj in mlist order from 1 (:362-371): its first jj factors
+                // are the running prefix pre[jj] -- the same roundings -- so only the
+                // factors after jj are multiplied per output (35 multiplies, not 56)
+                F pre[DC];
+                pre[0] = F(1);
+#pragma unroll
+                for (int k = 0; k + 1 < DC; ++k) pre[k + 1] = pre[k] * th[k];
 #pragma unroll
                 for (int jj = 0; jj < DC; ++jj) {
-                    F prod = F(1);
+                    F prod = pre[jj];
 #pragma unroll
-                    for (int k = 0; k < DC; ++k)
-                        if (k != jj) prod *= th[k];
+                    for (int k = jj + 1; k < DC; ++k) prod *= th[k];
                     F o = bp_log((F(1) + prod) / (F(1) - prod));
                     if (sizeof(F) == 4 && bp_abs(o) > maxllr) o = o >= F(0) ? maxllr : -maxllr;
                     prev[r][jj] = o;
