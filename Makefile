@@ -105,6 +105,13 @@ gdbfvariant: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/gdbf.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/gdbf.o
 
+# BP kernel A/B variants: make bpvariant NAME=x VFLAGS="-DLDPC_BP_..." -> lib/variants/libldpc_hip_x.so
+bpvariant: $(OBJS)
+	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/bp.o $(CSRC)/bp.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/bp.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/bp.o
+
 oracle:
 	$(MAKE) -f oracle/Makefile
 

@@ -217,8 +217,11 @@ static bool bp_rows_fits(const DevGraph &g, int E, bool f64)
     return L.total <= 150 * 1024 && (size_t)g.M * 8 * 2 <= (size_t)(L.total - L.msg_off);   // + the prologue's slot map
 }
 
+#ifndef LDPC_BP_ROWS_WAVES
+#define LDPC_BP_ROWS_WAVES 8   // 512-thread fp32 instance: 64 VGPRs, 4 workgroups per CU (11.9 vs 14.2 ms at 4)
+#endif
 template <typename F, int SRC, int NT>
-__global__ __launch_bounds__(NT, NT == 512 ? 4 : 2) void k_bp_rows(DecodeArgs a, DevGraph g, int msg_off, int E)
+__global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVES : 4) void k_bp_rows(DecodeArgs a, DevGraph g, int msg_off, int E)
 {
     constexpr int DC = 8, RPT = 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
