@@ -385,7 +385,7 @@ static GdbfRowsLayout gdbf_rows_layout(int N, int M, int fsz)
     GdbfRowsLayout L;
     L.np = ((N + 3) & ~3) + 4;                // d < 0 flags [0..N) + pad; the last word: dummy bits (0)
     L.soff = (L.np + 7) & ~7;
-    L.floff = L.soff + ((M + 1) * fsz + 7) / 8 * 8;   // w*s[0..M) as F, [M] = the dummy check (-0.0)
+    L.floff = L.soff + ((M + 2 + (M >> 5)) * fsz + 7) / 8 * 8;   // w*s at sidx(j), sidx(M) = the dummy check (-0.0)
     L.total = L.floff + 16;                   // flags[2] (+ pad)
     return L;
 }
@@ -410,6 +410,11 @@ static GdbfRowsLayout gdbf_rows_layout(int N, int M, int fsz)
 #ifndef LDPC_GDBF_ROWS_WAVES64
 #define LDPC_GDBF_ROWS_WAVES64 4
 #endif
+// LDS index of check j's term: one pad word per 32, so the stride-4 rows that
+// the lanes of a bit slot read (bits 4t + q of a quasi-cyclic block) fall in
+// distinct banks (measured 4-way conflicts with the plain index)
+__device__ __forceinline__ uint32_t sidx(uint32_t j) { return j + (j >> 5); }
+
 template <typename F, int SRC, int DVM, int NT>
 __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS_WAVES : LDPC_GDBF_ROWS_WAVES64) void k_gdbf_rows(GdbfArgs a, DevGraph g, int np, int soff, int floff)
 {
@@ -454,7 +459,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
         for (int k = 0; k < DVM; k += 2) {
             const uint32_t j0 = k < deg ? g.col_refs[e0 + k] >> 6 : (uint32_t)M;
             const uint32_t j1 = k + 1 < deg ? g.col_refs[e0 + k + 1] >> 6 : (uint32_t)M;
-            bc[q][k / 2] = j0 | (j1 << 16);
+            bc[q][k / 2] = sidx(j0) | (sidx(j1) << 16);
         }
         int m = deg;
 #pragma unroll
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
     }
     if (tid == 0) {
         *reinterpret_cast<uint32_t *>(dl + np - 4) = 0u;   // dummy bits: d = +1
-        sl[M] = -F(0);                                      // dummy check: E + -0.0 == E for every E
+        sl[sidx(M)] = -F(0);                                // dummy check: E + -0.0 == E for every E
     }
     const bool smooth = (a.flags & GDBF_SMOOTH) != 0, noise = (a.flags & GDBF_NOISE) != 0;
     const bool adapt = (a.flags & GDBF_ADAPT) != 0;
@@ -581,7 +586,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
                 uint32_t p = 0;
 #pragma unroll
                 for (int k = 0; k < DC; ++k) p ^= g8[r][k];
-                if (rvalid[r]) sl[tid + r * NT] = w * (p ? F(-1) : F(1));   // w * (F)s_j, as :541-551 adds it
+                if (rvalid[r]) sl[sidx(tid + r * NT)] = w * (p ? F(-1) : F(1));   // w * (F)s_j, as :541-551 adds it
                 fail |= (int)p;
             }
             if (fail) fl[it & 1] = 1;
