@@ -12,7 +12,7 @@ HIPFLAGS  = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iincl
 CXXFLAGS  = -O2 -std=c++17 -ffp-contract=off -Iinclude -Wall
 
 LIB       = $(LIBDIR)/libldpc_hip.so
-OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
+OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
 CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalizedMinSum $(BINDIR)/decodeOffsetMinSum \
             $(BINDIR)/decodeMNGDBF $(BINDIR)/decodeSMNGDBF $(BINDIR)/decodeATGDBF $(BINDIR)/decodeSATGDBF $(BINDIR)/decodeSMGDBF $(BINDIR)/decodeBP \
             $(BINDIR)/decodeSGDBF $(BINDIR)/decodeMGDBF $(BINDIR)/decodeStochasticNGDBF
@@ -29,7 +29,9 @@ $(BINDIR):
 KERNFLAGS = -Xclang -target-feature -Xclang -load-store-opt
 $(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
-$(LIBDIR)/obj/rows_fast.o: $(CSRC)/rows_fast.hip $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
+$(LIBDIR)/obj/rows_fast.o: $(CSRC)/rows_fast.hip $(CSRC)/fast64.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
+$(LIBDIR)/obj/rows_pp.o: $(CSRC)/rows_pp.hip $(CSRC)/fast64.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -89,7 +91,7 @@ variant:
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/api.o $(CSRC)/api.cpp
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/graph.o
+	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/graph.o
 
 # Fast row kernel A/B variants: make fastvariant NAME=x VFLAGS="-DLDPC_FAST_..." -> lib/variants/libldpc_hip_x.so
 fastvariant: $(OBJS)
@@ -97,6 +99,13 @@ fastvariant: $(OBJS)
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_fast.o $(CSRC)/rows_fast.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/rows_fast.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/rows_fast.o
+
+# Ping-pong kernel A/B variants: make ppvariant NAME=x VFLAGS="-DLDPC_PP_..." -> lib/variants/libldpc_hip_x.so
+ppvariant: $(OBJS)
+	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o $(CSRC)/rows_pp.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/rows_pp.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o
 
 # GDBF kernel A/B variants: make gdbfvariant NAME=x VFLAGS="-DLDPC_GDBF_..." -> lib/variants/libldpc_hip_x.so
 gdbfvariant: $(OBJS)
@@ -122,7 +131,7 @@ ref:
 clean:
 	rm -rf $(LIBDIR) $(BINDIR) oracle/liboracle.so
 
-.PHONY: all oracle ref clean variant fastvariant
+.PHONY: all oracle ref clean variant fastvariant ppvariant
 
 # Host-code sanitizer build: graph.cpp (the Tanner-graph compiler)
 # and the CPU oracle under AddressSanitizer + UBSan, driven over code files.

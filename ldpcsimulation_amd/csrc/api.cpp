@@ -530,6 +530,16 @@ static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool 
            ldpc::redo_lds_bytes(c->dg, f64) <= 160 * 1024;
 }
 
+// fp64 on the fast path: the ping-pong kernel (two codewords per block, check
+// and bit waves overlapped) when the schedule fits it; LDPC_ROWS=fast keeps
+// the one-codeword-per-block k_rows_fast. Opt-in (LDPC_ROWS=pp) until measured.
+static bool use_rows_pp(const ldpc_ctx *c, bool f64)
+{
+    const char *env = std::getenv("LDPC_ROWS");
+    if (!f64 || !(env && std::strcmp(env, "pp") == 0)) return false;
+    return ldpc::rows_pp_supported(c->dg, c->rs);
+}
+
 // Flooding of codes beyond LDS: one launch per phase over an Infinity-Cache-
 // resident set (default; 1.5x the persistent kernel on DVB-S2) or the
 // persistent workgroup-per-codeword kernel (LDPC_FLOOD_MODE=persistent).
@@ -594,8 +604,11 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
     c->last_fast = fast;
     if (fast) {
         HIP_TRY(hipMemsetAsync(c->redo.p, 0, sizeof(unsigned), c->stream));
-        HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, f64, kc.lds_bytes, (unsigned *)c->redo.p, c->stream,
-                                       c->num_cus));
+        if (use_rows_pp(c, f64))
+            HIP_TRY(ldpc::launch_rows_pp(c->dg, c->rs, a, (unsigned *)c->redo.p, c->stream, c->num_cus));
+        else
+            HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, f64, kc.lds_bytes, (unsigned *)c->redo.p, c->stream,
+                                           c->num_cus));
         HIP_TRY(ldpc::launch_redo(c->dg, a, f64, (const unsigned *)c->redo.p, c->stream, c->num_cus));
     } else if (layered) {
         HIP_TRY(ldpc::launch_layered(c->dg, a, f64, kc, c->fs, c->ls, c->gscratch.p, gblocks, c->stream));
@@ -931,7 +944,9 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     rc = nms_setup(c, cfg, a);   // fp32 NMS: whether the verified reciprocal (and so the fast kernel) applies
     if (rc) return rc;
     if (name && name_len > 0)
-        std::snprintf(name, (size_t)name_len, "%s", cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64, a) ? "rows_fast" : kc.name);
+        std::snprintf(name, (size_t)name_len, "%s",
+                      cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64, a) ? (use_rows_pp(c, f64) ? "rows_pp" : "rows_fast")
+                                                                                : kc.name);
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
     if (bpc) *bpc = cfg->variant == LDPC_BP ? 0 : is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
                                    : ldpc::blocks_per_cu(c->dg, f64, kc);

@@ -23,7 +23,7 @@
 //                  on the GPU, so the output equals the reference's.
 //                  philox: channel and perturbations generated on the GPU,
 //                  batched (LDPC_BATCH frames per launch).
-//   LDPC_SEED, LDPC_PRECISION, LDPC_BATCH, LDPC_DEVICE as cli_minsum.cpp.
+//   LDPC_SEED, LDPC_PRECISION, LDPC_BATCH, LDPC_DEVICE, LDPC_DRY_RUN as cli_minsum.cpp.
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -228,7 +228,7 @@ int main(int argc, char *argv[])
         std::cerr << "ldpc: LDPC_RNG must be glibc or philox" << endl;
         return 1;
     }
-    const std::string prec = env_or("LDPC_PRECISION", philox ? "f32" : "f64");
+    const std::string prec = env_or("LDPC_PRECISION", "f64");   // the reference's double; f32 opt-in
     cfg.precision = prec == "f32" ? LDPC_F32 : LDPC_F64;
     const long long seed = std::atoll(env_or("LDPC_SEED", std::to_string((long long)time(0)).c_str()));
     const int batch = philox ? std::atoi(env_or("LDPC_BATCH", "65536")) : 1;
@@ -236,6 +236,11 @@ int main(int argc, char *argv[])
     if (batch <= 0) {
         std::cerr << "ldpc: LDPC_BATCH must be > 0" << endl;
         return 1;
+    }
+    if (std::getenv("LDPC_DRY_RUN")) {   // report the GPU settings and stop before any device call
+        std::cerr << "ldpc: rng=" << rng << " precision=" << (cfg.precision == LDPC_F64 ? "f64" : "f32")
+                  << " batch=" << batch << " device=" << device << endl;
+        return 0;
     }
     ldpc_ctx *ctx = nullptr;
     if (ldpc_ctx_create(device, H, batch, &ctx) != LDPC_OK) die("creating device context");

@@ -21,9 +21,10 @@
 //                  output then equals the reference's for the same seed.
 //                  philox: counter-based noise generated on the GPU.
 //   LDPC_SEED      noise seed (default time(0), as ran_seed(time(0)) :187)
-//   LDPC_PRECISION f64 | f32 (default f64 for glibc, f32 for philox)
+//   LDPC_PRECISION f64 (default: the reference's double) | f32 (opt-in)
 //   LDPC_BATCH     frames per GPU launch (default 512 glibc / 65536 philox)
 //   LDPC_DEVICE    HIP device index (default 0)
+//   LDPC_DRY_RUN   print these settings to stderr and exit before any device call
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
@@ -191,7 +192,7 @@ int main(int argc, char *argv[])
         std::cerr << "ldpc: LDPC_RNG must be glibc or philox" << endl;
         return 1;
     }
-    const std::string prec = env_or("LDPC_PRECISION", philox ? "f32" : "f64");
+    const std::string prec = env_or("LDPC_PRECISION", "f64");
     cfg.precision = prec == "f32" ? LDPC_F32 : LDPC_F64;
     const long long seed = std::atoll(env_or("LDPC_SEED", std::to_string((long long)time(0)).c_str()));
     const int batch = std::atoi(env_or("LDPC_BATCH", philox ? "65536" : "512"));
@@ -199,6 +200,11 @@ int main(int argc, char *argv[])
     if (batch <= 0) {
         std::cerr << "ldpc: LDPC_BATCH must be > 0" << endl;
         return 1;
+    }
+    if (std::getenv("LDPC_DRY_RUN")) {   // report the GPU settings and stop before any device call
+        std::cerr << "ldpc: rng=" << rng << " precision=" << (cfg.precision == LDPC_F64 ? "f64" : "f32")
+                  << " batch=" << batch << " device=" << device << endl;
+        return 0;
     }
     ldpc_ctx *ctx = nullptr;
     if (ldpc_ctx_create(device, H, batch, &ctx) != LDPC_OK) die("creating device context");

@@ -1,0 +1,488 @@
+// rows_pp.hip -- the fp64 headline kernel: flooding min-sum (src/decodeMinSum.cpp
+// :247-263, check node :410-450, normalisation :494-515, bit node :452-476)
+// with check and bit work of two codewords overlapped in one workgroup.
+//
+// k_rows_fast (rows_fast.hip) decodes one codeword per 512-thread block; inside
+// a block the check phase (VALU-heavy: the f64 tournament, division, selects)
+// and the bit phase (LDS-latency-bound: c2v reads and dependent adds) alternate
+// between barriers, so a CU's VALU and LDS pipe are each busy only about half
+// the time. Here one 1024-thread block holds TWO
+// codewords (slots 0 and 1, 2 x 74 KB of LDS for N=1944) and its waves are
+// specialised:
+//   waves 0-7  (the check role) own check rows t and t+512, as k_rows_fast's
+//              threads do, with their schedule in registers;
+//   waves 8-15 (the bit role) own the bit slots of k_rows_fast's thread t-512.
+// Between two barriers the check role runs iteration i of one slot while the
+// bit role runs the bit nodes of the other slot:
+//   | check(0,0) | check(1,0)  | check(0,1)  | ... | check(1,T-1) |             |
+//   |            | bit(0,0)    | bit(1,0)    | ... | bit(0,T-1)   | bit(1,T-1)  |
+// so every interval carries one check phase and one bit phase, on different
+// waves of the same SIMDs: 2T + 1 barrier intervals per pair instead of 4T.
+// A slot's check(i+1) follows its bit(i), which follows its check(i), each an
+// interval apart: the flooding schedule of each codeword is unchanged, and so
+// is every value (same arithmetic as k_rows_fast: cn_fast64 of fast64.h, sums
+// in nlist order), hence the decisions equal the reference's bit for bit.
+//
+// The c2v a row sent last iteration (the `- msg` of :469) is kept per slot in
+// registers (prev, 2 slots x 2 rows x 8 edges) or, with PREV_LDS, re-read from
+// the row's own c2v slots (8 more ds_read_b64 per row, 32 fewer VGPRs... the
+// default is the measured winner).
+//
+// Premise failures (fast64.h): the slot's flag is raised and the codeword is
+// re-decoded on the exact path (k_redo) after the launch; the other slot of
+// the pair is unaffected. Rows past M (degree 0) gather app[N + 2] = +0, so
+// their messages stay 0 (their scatters land in per-lane dummy slots that the
+// padding edges of real rows also use; those read +inf - finite = +inf).
+#include "kernels.h"
+#include "device_common.h"
+#include "minsum_common.h"
+#include "fast64.h"
+
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <type_traits>
+
+namespace ldpc {
+
+namespace {
+
+// Timing experiments only (wrong results; `make ppvariant`): LDPC_PP_EXP =
+// 1 bit role idle (barriers only), 2 check role idle, 3 check node replaced by
+// a subtraction, 4 no c2v scatters.
+#ifndef LDPC_PP_EXP
+#define LDPC_PP_EXP 0
+#endif
+
+// Wave priority (s_setprio): 0 none, 1 check role above the bit role, 2 the reverse.
+#ifndef LDPC_PP_PRIO
+#define LDPC_PP_PRIO 0
+#endif
+// 1: the check role issues both rows' LDS reads before computing row 0; 0: row 1's after it.
+#ifndef LDPC_PP_PREFETCH
+#define LDPC_PP_PREFETCH 1
+#endif
+
+// Diagnostic builds (-DLDPC_STAMPS, `make ppvariant`): per wave, s_memtime cycles
+// spent working and waiting at the interval barriers, to a.stamps[(block*16+wave)*2].
+#ifdef LDPC_STAMPS
+#define PP_STAMP_DECL unsigned long long st_work = 0, st_wait = 0, st_t0 = __builtin_amdgcn_s_memtime()
+#define PP_BARRIER()                                                        \
+    do {                                                                    \
+        const unsigned long long te_ = __builtin_amdgcn_s_memtime();        \
+        __syncthreads();                                                    \
+        const unsigned long long tb_ = __builtin_amdgcn_s_memtime();        \
+        st_work += te_ - st_t0;                                             \
+        st_wait += tb_ - te_;                                               \
+        st_t0 = tb_;                                                        \
+    } while (0)
+#define PP_STAMP_OUT()                                                                              \
+    if (a.stamps && (threadIdx.x & 63) == 0 && blockIdx.x < 256) {                                  \
+        a.stamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 2] = st_work;                             \
+        a.stamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 2 + 1] = st_wait;                         \
+    }
+#else
+#define PP_STAMP_DECL
+#define PP_BARRIER() __syncthreads()
+#define PP_STAMP_OUT()
+#endif
+
+constexpr int kPPRole = 512;          // threads per role
+constexpr int kPPRedInts = 160;       // [0,2): slot flags; [32,128): block sums; [128,140): acc (6 x u64)
+
+struct PPSlots {
+    Pack<double, 1> *app[2], *c2v[2];
+    uint32_t app_base[2], c2v_base[2];   // LDS byte addresses
+    int *red;
+};
+
+__device__ __forceinline__ PPSlots pp_slots(unsigned char *smem, int N, int EA)
+{
+    using P = Pack<double, 1>;
+    PPSlots s;
+    const int SL = N + 3 + EA;
+    P *b = reinterpret_cast<P *>(smem);
+#pragma unroll
+    for (int X = 0; X < 2; ++X) {
+        s.app[X] = b + X * SL;
+        s.c2v[X] = s.app[X] + (N + 3);
+        s.app_base[X] = lds_addr_of(s.app[X]);
+        s.c2v_base[X] = lds_addr_of(s.c2v[X]);
+    }
+    s.red = reinterpret_cast<int *>(b + 2 * SL);
+    return s;
+}
+
+// Channel of the pair (:214-238) staged into app[X][v] (v < N), by all 1024
+// threads, 4 bits (one Philox call) per thread and step; unc[X] = this thread's
+// uncoded errors of slot X.
+template <int SRC>
+__device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots &s, int N, int grp, int (&unc)[2])
+{
+    using F = double;
+    unc[0] = unc[1] = 0;
+    const int ng4 = (N + 3) / 4;
+    for (int t = threadIdx.x; t < 2 * ng4; t += blockDim.x) {
+        const int X = t >= ng4 ? 1 : 0, g4 = t - X * ng4;
+        const int b = grp * 2 + X;
+        if (b >= a.batch) continue;
+        const uint64_t cw = a.first_cw + (uint64_t)b;
+        Pack<double, 1> *ap = s.app[X];
+        F yv[4];
+        const int8_t *cvec;
+        if (SRC == SRC_GIVEN) {
+            cvec = a.c ? a.c + (size_t)b * N : nullptr;
+            const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) yv[q4] = 4 * g4 + q4 < N ? y[4 * g4 + q4] : F(0);
+        } else {
+            cvec = a.cw_table ? a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N : nullptr;
+            uint32_t u[4];
+            philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, (uint32_t)a.seed,
+                          (uint32_t)(a.seed >> 32), u);
+            F n[4];
+            box_muller(u[0], u[1], n[0], n[1]);
+            box_muller(u[2], u[3], n[2], n[3]);
+            const F sigma = (F)a.sigma;
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) {
+                const int v = 4 * g4 + q4;
+                const int cv = (cvec && v < N) ? cvec[v] : 1;
+                yv[q4] = (F)cv * (F(1) + sigma * n[q4]);
+                if (a.y_out && v < N) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv[q4];
+            }
+        }
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+            const int v = 4 * g4 + q4;
+            if (v < N) {
+                const int cv = cvec ? cvec[v] : 1;
+                const F q = front_end<F>(yv[q4], a);
+                ap[v].v[0] = q;
+                const int e = ((q > F(0) ? 1 : -1) * cv < 0);
+                unc[0] += X ? 0 : e;
+                unc[1] += X ? e : 0;
+            }
+        }
+    }
+}
+
+// Block sums of the pair's (bit errors, uncoded errors, syndrome) and the
+// per-codeword accounting (:270-288, :382-393) by thread 0; premise failures
+// go to the re-decode list instead.
+__device__ __forceinline__ void pp_account(const DecodeArgs &a, const PPSlots &s, int grp, int (&sums)[6],
+                                           unsigned *redo, unsigned long long *acc)
+{
+    block_sum_n<6>(sums, s.red + 32);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int X = 0; X < 2; ++X) {
+            const int b = grp * 2 + X;
+            if (b >= a.batch) continue;
+            if (s.red[X]) {
+                s.red[X] = 0;   // read once per pair; raised again only after the next B1
+                const unsigned at = atomicAdd(&redo[0], 1u);
+                redo[1 + at] = (unsigned)b;
+                continue;
+            }
+            const int w = sums[3 * X], uc = sums[3 * X + 1], sf = sums[3 * X + 2] > 0;
+            acc[0] += (unsigned long long)w;
+            acc[1] += (unsigned long long)(w > 0);
+            acc[2] += (unsigned long long)uc;
+            acc[3] += 1ull;
+            acc[5] += (unsigned long long)sf;
+            if (w > 0 && a.hist) atomicAdd(&a.hist[w - 1], 1ull);
+            if (a.frame_res) a.frame_res[b] = make_int4(w, uc, sf, 0);
+        }
+    }
+}
+
+// ---- the check role: rows t and t + 512 of both slots ----
+template <int SRC, int DC, int VAR, bool FDIV, bool PREV_LDS>
+__device__ __forceinline__ void pp_check_role(const DecodeArgs &a, const DevGraph &g, const RowSched &rs,
+                                              const PPSlots &s, unsigned *redo, unsigned long long *acc)
+{
+    using P = Pack<double, 1>;
+    constexpr int RPT = 2;
+    const int tid = threadIdx.x, N = g.N;
+    int deg[RPT];
+    uint32_t colw[RPT][DC / 2], posw[RPT][DC / 2];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+        const int j = tid + r * kPPRole;
+        deg[r] = rs.cn_deg[j];
+#pragma unroll
+        for (int q = 0; q < DC / 8; ++q) {
+            const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)j * DC)[q];
+            const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)j * DC)[q];
+            colw[r][4 * q + 0] = xc.x; colw[r][4 * q + 1] = xc.y; colw[r][4 * q + 2] = xc.z; colw[r][4 * q + 3] = xc.w;
+            posw[r][4 * q + 0] = xp.x; posw[r][4 * q + 1] = xp.y; posw[r][4 * q + 2] = xp.z; posw[r][4 * q + 3] = xp.w;
+        }
+        if (deg[r] == 0)   // rows past M: gather the +0 entry, so their messages stay 0
+#pragma unroll
+            for (int q = 0; q < DC / 2; ++q) colw[r][q] = (uint32_t)(N + 2) * 0x10001u;
+    }
+    const double alpha = a.alpha, delta = a.delta, rcp = 1.0 / a.alpha;
+    const int npairs = (a.batch + 1) / 2;
+    [[maybe_unused]] P prev[2][RPT][DC];
+    PP_STAMP_DECL;
+    for (int grp = blockIdx.x; grp < npairs; grp += gridDim.x) {
+        int unc[2];
+        pp_channel<SRC>(a, s, N, grp, unc);
+        __syncthreads();   // B1: channel staged
+        if constexpr (!PREV_LDS) {
+#pragma unroll
+            for (int X = 0; X < 2; ++X)
+#pragma unroll
+                for (int r = 0; r < RPT; ++r)
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) prev[X][r][k].v[0] = 0.0;
+        }
+        __syncthreads();   // B2: yq in app, padding slots zeroed (bit role)
+
+        // check nodes of slot X (row 1's reads issued before row 0 is computed)
+        auto check = [&](auto Xc) {
+            constexpr int X = decltype(Xc)::value;
+#pragma unroll
+            for (int r = 0; r < RPT; ++r)
+#pragma unroll
+                for (int q = 0; q < DC / 2; ++q) asm volatile("" : "+v"(colw[r][q]), "+v"(posw[r][q]));
+            const uint32_t ab = s.app_base[X], cb = s.c2v_base[X];
+            P xin[RPT][DC];
+            [[maybe_unused]] P pv[RPT][DC];
+            auto reads = [&](int r) {
+#pragma unroll
+                for (int k = 0; k < DC; ++k) xin[r][k] = lds_at<P>(addr8<DC>(colw[r], k, ab));
+                if constexpr (PREV_LDS) {
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) pv[r][k] = lds_at<P>(addr8<DC>(posw[r], k, cb));
+                }
+            };
+#pragma unroll
+            for (int r = 0; r < (LDPC_PP_PREFETCH ? RPT : 1); ++r) reads(r);
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) {
+                if (!LDPC_PP_PREFETCH && r > 0) reads(r);
+                P(&pr)[DC] = PREV_LDS ? pv[r] : prev[X][r];
+                bool ok = true;
+                if constexpr (LDPC_PP_EXP == 3) {
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) pr[k].v[0] = xin[r][k].v[0] - pr[k].v[0];
+                } else {
+                    ok = cn_fast64<DC, VAR, FDIV>(xin[r], pr, alpha, rcp, delta);
+                }
+                if (!ok && deg[r] > 0) s.red[X] = 1;
+                if constexpr (LDPC_PP_EXP != 4) {
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) lds_put<P>(addr8<DC>(posw[r], k, cb), pr[k]);
+                }
+                __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
+            }
+        };
+        for (int it = 0; it < a.T; ++it) {
+            if (LDPC_PP_EXP != 2) check(std::integral_constant<int, 0>());
+            PP_BARRIER();   // | check(0,it) | bit(1,it-1) |
+            if (LDPC_PP_EXP != 2) check(std::integral_constant<int, 1>());
+            PP_BARRIER();   // | check(1,it) | bit(0,it) |
+        }
+        if (a.T > 0) PP_BARRIER();   // | -- | bit(1,T-1) |
+
+        // syndrome of both slots (padding edges read +inf: parity 0; rows past M skipped)
+        int sums[6] = {0, unc[0], 0, 0, unc[1], 0};
+#pragma unroll
+        for (int X = 0; X < 2; ++X) {
+            int synd = 0;
+#pragma unroll
+            for (int r = 0; r < RPT; ++r) {
+                int par = 0;
+#pragma unroll
+                for (int k = 0; k < DC; ++k) par ^= (s.app[X][u16_at<DC>(colw[r], k)].v[0] > 0.0) ? 0 : 1;
+                synd |= deg[r] > 0 ? par : 0;
+            }
+            sums[3 * X + 2] = synd;
+        }
+        pp_account(a, s, grp, sums, redo, acc);
+    }
+    PP_STAMP_OUT()
+}
+
+// ---- the bit role: the bit slots of row-schedule thread t - 512, both slots ----
+template <int SRC, int CPT>
+__device__ __forceinline__ void pp_bit_role(const DecodeArgs &a, const DevGraph &g, const RowSched &rs,
+                                            const PPSlots &s, unsigned *redo, unsigned long long *acc, bool prev_lds)
+{
+    using P = Pack<double, 1>;
+    const int bt = threadIdx.x - kPPRole, N = g.N, lane = threadIdx.x & 63;
+    int vgb[CPT], vgd[CPT];
+    uint32_t vdst2[(CPT + 1) / 2] = {};
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int c = rs.vn_col[bt * CPT + i];
+        vdst2[i / 2] |= (uint32_t)(c == 0xffff ? N + 1 : c) << (16 * (i & 1));
+        const uint32_t info = rs.vn_info[bt * CPT + i];
+        vgb[i] = __builtin_amdgcn_readfirstlane((int)(info & 0xffffu) - lane);
+        vgd[i] = __builtin_amdgcn_readfirstlane((int)(info >> 24));
+    }
+    auto vdst = [&](int i) -> int { return (int)((vdst2[i / 2] >> (16 * (i & 1))) & 0xffffu); };
+    const int EA = rs.e_pad + 64;
+    if (!prev_lds) {   // padding slots of the bit-node layout hold +0 (adding +0 changes no sum); never written
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int dg = (int)((rs.vn_info[bt * CPT + i] >> 16) & 0xffu);
+            const int base = vgb[i] + lane, gd = vgd[i];
+            for (int k = dg; k < gd; ++k) s.c2v[0][base + k * 64].v[0] = s.c2v[1][base + k * 64].v[0] = 0.0;
+        }
+    }
+    const int npairs = (a.batch + 1) / 2;
+    PP_STAMP_DECL;
+    for (int grp = blockIdx.x; grp < npairs; grp += gridDim.x) {
+        int unc[2];
+        pp_channel<SRC>(a, s, N, grp, unc);
+        if (prev_lds) {   // the check role re-reads its last messages: all c2v slots start at +0
+            for (int e = bt; e < EA; e += kPPRole) s.c2v[0][e].v[0] = s.c2v[1][e].v[0] = 0.0;
+        }
+        __syncthreads();   // B1
+        P yq[2][CPT];
+#pragma unroll
+        for (int X = 0; X < 2; ++X) {
+            bool in_ok = true;
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                // yq + 0 maps -0 to +0, so app is never -0 (fast64.h premise)
+                yq[X][i].v[0] = s.app[X][vdst(i) <= N ? vdst(i) : 0].v[0] + 0.0;
+                in_ok &= __builtin_fabs(yq[X][i].v[0]) < kFast64Max;
+            }
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) s.app[X][vdst(i)] = yq[X][i];   // v2c = yq on the first pass (:364-370)
+            if (!in_ok) s.red[X] = 1;
+        }
+        if (threadIdx.x == kPPRole) s.app[0][N].v[0] = s.app[1][N].v[0] = __builtin_huge_val();
+        if (threadIdx.x == kPPRole + 1) s.app[0][N + 2].v[0] = s.app[1][N + 2].v[0] = 0.0;
+        __syncthreads();   // B2
+
+        // bit nodes of slot Y: sum = yq + c2v in nlist order (:452-476)
+        auto bits = [&](auto Yc) {
+            constexpr int Y = decltype(Yc)::value;
+#pragma unroll
+            for (int q = 0; q < (CPT + 1) / 2; ++q) asm volatile("" : "+v"(vdst2[q]));
+            P sum[CPT];
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) sum[i] = yq[Y][i];
+            int k = 0;
+            const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+            vn_phases<double, 1, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum);
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) s.app[Y][vdst(i)] = sum[i];
+        };
+        for (int it = 0; it < a.T; ++it) {
+            if (it > 0 && LDPC_PP_EXP != 1) bits(std::integral_constant<int, 1>());
+            PP_BARRIER();
+            if (LDPC_PP_EXP != 1) bits(std::integral_constant<int, 0>());
+            PP_BARRIER();
+        }
+        if (a.T > 0) {
+            if (LDPC_PP_EXP != 1) bits(std::integral_constant<int, 1>());
+            PP_BARRIER();
+        }
+
+        // decisions and error weight (:270, :382-393) of both slots
+        int sums[6] = {0, unc[0], 0, 0, unc[1], 0};
+#pragma unroll
+        for (int X = 0; X < 2; ++X) {
+            const int b = grp * 2 + X;
+            if (b >= a.batch) continue;
+            const int8_t *cvec = SRC == SRC_GIVEN ? (a.c ? a.c + (size_t)b * N : nullptr)
+                                                  : (a.cw_table ? a.cw_table + (size_t)((a.first_cw + (uint64_t)b) % (uint64_t)a.cw_rows) * N
+                                                                : nullptr);
+            int w = 0;
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {
+                const int v = vdst(i);
+                if (v < N) {
+                    const int d = s.app[X][v].v[0] > 0.0 ? 1 : -1;   // :471-474
+                    const int cv = cvec ? cvec[v] : 1;
+                    w += (d != cv);
+                    if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+                }
+            }
+            sums[3 * X] = w;
+        }
+        pp_account(a, s, grp, sums, redo, acc);
+    }
+    PP_STAMP_OUT()
+}
+
+}  // namespace
+
+template <int SRC, int DC, int CPT, int VAR, bool FDIV, bool PREV_LDS>
+__global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph g, RowSched rs, unsigned *redo)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const PPSlots s = pp_slots(smem, g.N, rs.e_pad + 64);
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(s.red + 128);   // thread 0's block totals
+    if (threadIdx.x == 0) {
+        s.red[0] = s.red[1] = 0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) acc[q] = 0;
+    }
+    // the role is wave-uniform (an SGPR branch), so both sides meet every barrier
+    const bool checker = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < kPPRole / 64;
+    if (LDPC_PP_PRIO == 1 && checker) __builtin_amdgcn_s_setprio(1);
+    if (LDPC_PP_PRIO == 2 && !checker) __builtin_amdgcn_s_setprio(1);
+    if (checker)
+        pp_check_role<SRC, DC, VAR, FDIV, PREV_LDS>(a, g, rs, s, redo, acc);
+    else
+        pp_bit_role<SRC, CPT>(a, g, rs, s, redo, acc, PREV_LDS);
+    if (threadIdx.x == 0 && acc[3] > 0) {
+        acc[4] = acc[3] * (unsigned long long)a.T;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) atomicAdd(&a.counts[q], acc[q]);
+    }
+}
+
+int rows_pp_lds_bytes(const DevGraph &g, const RowSched &rs)
+{
+    return (int)(2 * (size_t)(g.N + 3 + rs.e_pad + 64) * sizeof(double) + kPPRedInts * sizeof(int));
+}
+
+bool rows_pp_supported(const DevGraph &g, const RowSched &rs)
+{
+    return rs.threads == kPPRole && rs.rpt == 2 && rs.cpt == 4 && rs.dc == 8 && g.N + 3 <= 0xffff &&
+           rows_pp_lds_bytes(g, rs) <= 160 * 1024;
+}
+
+#ifndef LDPC_PP_PREV_LDS
+#define LDPC_PP_PREV_LDS 0
+#endif
+
+template <int SRC, int VAR, bool FDIV>
+static hipError_t launch_pp_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, unsigned *redo,
+                              hipStream_t s, int num_cus)
+{
+    const bool prev_lds = std::getenv("LDPC_PP_PREV") ? std::getenv("LDPC_PP_PREV")[0] == 'l' : LDPC_PP_PREV_LDS;
+    auto fn = prev_lds ? k_rows_pp<SRC, 8, 4, VAR, FDIV, true> : k_rows_pp<SRC, 8, 4, VAR, FDIV, false>;
+    const int lds = rows_pp_lds_bytes(g, rs);
+    hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    const int npairs = (a.batch + 1) / 2;
+    const int grid = std::min(num_cus, npairs);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(2 * kPPRole), lds, s, a, g, rs, redo);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_pp(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, unsigned *redo, hipStream_t s,
+                          int num_cus)
+{
+    if (!rows_pp_supported(g, rs)) return hipErrorInvalidValue;
+    const bool given = a.src == SRC_GIVEN;
+#define LDPC_PP_SRC(VARV, FD) \
+    return given ? launch_pp_t<SRC_GIVEN, VARV, FD>(g, rs, a, redo, s, num_cus) : launch_pp_t<SRC_PHILOX, VARV, FD>(g, rs, a, redo, s, num_cus);
+    if (a.variant == V_MS) { LDPC_PP_SRC(V_MS, false) }
+    if (a.variant == V_OMS) { LDPC_PP_SRC(V_OMS, false) }
+    if (markstein_exact_alpha(a.alpha)) { LDPC_PP_SRC(V_NMS, true) }
+    LDPC_PP_SRC(V_NMS, false)
+#undef LDPC_PP_SRC
+}
+
+}  // namespace ldpc

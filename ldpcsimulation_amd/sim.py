@@ -35,6 +35,7 @@ class PointResult:
     T: int
     counts: dict = field(default_factory=dict)
     rounds: int = 0
+    frames_decoded: int = 0             # frames decoded over all ranks, incl. those past the stop
     hist: Optional[np.ndarray] = None   # error_weight_hist (:173), exact-stop frames only
 
     @property
@@ -125,15 +126,31 @@ class _Comm:
         return np.concatenate([o.cpu().numpy() for o in out])
 
 
+def round_sizes(batch: int, first_round: Optional[int] = None):
+    """Frames per rank of rounds 0, 1, 2, ...: first_round (default min(batch, 1024)),
+    doubling up to batch. A low-SNR point stops near its 40th frame error after a
+    small first round instead of after batch x W frames; a high-SNR point reaches
+    full rounds after a few doublings."""
+    b = max(1, min(batch, first_round if first_round is not None else 1024))
+    while True:
+        yield b
+        b = min(batch, 2 * b)
+
+
 def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, ebn0_db: float,
                    batch: int, min_bit_err: int = 200, min_frame_err: int = 40,
                    max_frames: Optional[int] = None, exact_stop: bool = True, device=None,
-                   iters_in_frames: bool = False, launcher=None) -> PointResult:
+                   iters_in_frames: bool = False, launcher=None, first_round: Optional[int] = None) -> PointResult:
     """Run one SNR point to the reference's stop rule.
 
     run_batch(first_cw, n) must decode global frames first_cw..first_cw+n-1 on
     this rank and return their per-frame results (FRAME_DTYPE). All ranks of
     an initialised torch.distributed group must call this together.
+
+    Round k decodes b_k frames per rank (round_sizes: first_round doubling up to
+    batch). The global frames are still consumed in order -- round k covers
+    [sum_{j<k} b_j W, sum_{j<=k} b_j W), rank r the r-th block of b_k -- so the
+    totals (exact_stop) equal a frame-by-frame run for any W, batch and first_round.
 
     launcher (optional, e.g. AsyncLauncher): launch(slot, first_cw, n) starts a
     round without waiting and collect(slot) returns its frames. Then, once the
@@ -149,31 +166,46 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
     rnd = 0
     ahead = False          # round rnd already launched (into slot rnd % 2)
     last = None            # the previous round's all-reduced increments
+    sizes, starts = [], [0]    # frames per rank of each round; global first frame of each round
+    gen = round_sizes(batch, first_round)
+    decoded = 0
+
+    def size_of(r):
+        while len(sizes) <= r:
+            sizes.append(next(gen))
+            starts.append(starts[-1] + sizes[-1] * comm.world)
+        return sizes[r]
 
     def first_of(r):
-        return r * batch * comm.world + comm.rank * batch
+        b = size_of(r)
+        return starts[r] + comm.rank * b
 
     while not stop_reached(acc[0], acc[1], min_bit_err, min_frame_err):
         if max_frames is not None and acc[3] >= max_frames:
             break
         first = first_of(rnd)
         if launcher is None:
-            fr = np.ascontiguousarray(run_batch(first, batch))
+            fr = np.ascontiguousarray(run_batch(first, size_of(rnd)))
         else:
             if not ahead:
-                launcher.launch(rnd % 2, first, batch)
-            # launch the next round now when it is surely needed: two more rounds like the last one
-            # stay below the stop rule and the frame cap (the decision is the same on every rank)
-            ahead = last is not None and not stop_reached(acc[0] + 2 * last[0], acc[1] + 2 * last[1],
-                                                          min_bit_err, min_frame_err) and \
-                (max_frames is None or acc[3] + 2 * last[3] < max_frames)
+                launcher.launch(rnd % 2, first, size_of(rnd))
+            # launch the next round now when it is surely needed: this round, scaled from the
+            # last one by its size, twice over stays below the stop rule and the frame cap
+            # (the decision is the same on every rank)
+            if last is not None:
+                g = 2.0 * size_of(rnd) / size_of(rnd - 1)
+                ahead = not stop_reached(acc[0] + g * last[0], acc[1] + g * last[1], min_bit_err, min_frame_err) \
+                    and (max_frames is None or acc[3] + g * last[3] < max_frames)
+            else:
+                ahead = False
             if ahead:
-                launcher.launch((rnd + 1) % 2, first_of(rnd + 1), batch)
+                launcher.launch((rnd + 1) % 2, first_of(rnd + 1), size_of(rnd + 1))
             fr = np.ascontiguousarray(launcher.collect(rnd % 2))
         raw = fr.view(np.int32).reshape(-1, 4)
         local = np.array([raw[:, 0].sum(), (raw[:, 0] > 0).sum(), raw[:, 1].sum(), len(raw),
                           raw[:, 3].sum() if iters_in_frames else T * len(raw), raw[:, 2].sum()], dtype=np.int64)
         tot = comm.allreduce_sum(local)
+        decoded += int(tot[3])
         last = tot
         after = acc + tot
         crossed = stop_reached(after[0], after[1], min_bit_err, min_frame_err)
@@ -191,10 +223,11 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
             np.add.at(hist_local, w[w > 0] - 1, 1)
         rnd += 1
     if launcher is not None and ahead:
-        launcher.collect(rnd % 2)   # drain the round launched ahead of the stop (discarded)
+        decoded += len(launcher.collect(rnd % 2)) * comm.world   # drain the round launched past the stop
     hist = comm.allreduce_sum(hist_local) + hist_cut
     res.counts = dict(zip(COUNT_KEYS, (int(x) for x in acc)))
     res.rounds = rnd
+    res.frames_decoded = decoded
     res.hist = hist
     return res
 

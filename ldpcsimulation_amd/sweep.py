@@ -45,10 +45,13 @@ def parse(argv=None):
     p.add_argument("--delta", type=float, default=0.0)
     p.add_argument("--quantize", nargs=2, metavar=("YMAX", "Q"), help="-D quantizeSamples front-end")
     p.add_argument("--saturate", type=float, metavar="YMAX", help="-D saturateSamples front-end")
-    p.add_argument("--precision", choices=["f32", "f64"], default="f32")
+    p.add_argument("--precision", choices=["f32", "f64"], default="f64",
+                   help="f64 = the reference's double (default); f32 = the fp32 kernels (opt-in)")
     p.add_argument("--schedule", choices=["flooding", "layered"], default="flooding",
                    help="flooding = the reference's schedule; layered = row-serial (BASELINE config 3)")
-    p.add_argument("--batch", type=int, default=65536, help="frames per GPU per round")
+    p.add_argument("--batch", type=int, default=65536, help="frames per GPU per round (the largest round)")
+    p.add_argument("--first-round", type=int, default=None,
+                   help="frames per GPU in the first round; rounds double up to --batch (default min(batch, 1024))")
     p.add_argument("--seed", type=int, default=None, help="noise seed (default: time)")
     p.add_argument("--min-bit-errors", type=int, default=200)
     p.add_argument("--min-frame-errors", type=int, default=None,
@@ -63,6 +66,10 @@ def parse(argv=None):
     p.add_argument("--json", action="store_true", help="also print one JSON object per point")
     p.add_argument("--sync", action="store_true",
                    help="one blocking round at a time (default: the next round decodes while one is reduced)")
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="collective backend for world > 1 (nccl = RCCL over xGMI; gloo: CPU tensors)")
+    p.add_argument("--share-device", action="store_true",
+                   help="every rank on device 0 (rehearsal of N ranks on one GPU, with --backend gloo)")
     return p.parse_args(argv)
 
 
@@ -71,20 +78,25 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    device = local if world > 1 else 0
+    device = local if world > 1 and not a.share_device else 0
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(device)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
     seed = a.seed if a.seed is not None else int(time.time())
     if world > 1 and a.seed is None:
         # every rank must key its noise with rank 0's seed (ranks may start in different seconds)
         import torch
         import torch.distributed as dist
-        t = torch.tensor([seed], dtype=torch.int64, device=f"cuda:{device}")
+        t = torch.tensor([seed], dtype=torch.int64, device=f"cuda:{device}" if a.backend == "nccl" else "cpu")
         dist.broadcast(t, src=0)
         seed = int(t.item())
+    if os.environ.get("LDPC_SWEEP_REPORT_SEED"):   # tests: every rank reports the seed it keys its noise with
+        print(json.dumps({"rank": rank, "seed": seed}), file=sys.stderr, flush=True)
     if a.ems:
         return _ems_sweep(a, seed, world, rank, device)
     cfg = native.DecoderConfig(variant=VARIANTS[a.variant], T=a.iterations, alpha=a.alpha, delta=a.delta,
@@ -122,7 +134,7 @@ def main(argv=None) -> int:
             launcher = sim.AsyncLauncher(ctx, a.batch, run_launch)
         t0 = time.perf_counter()
         res = sim.simulate_point(run_batch, g.N, a.iterations, snr, a.batch, a.min_bit_errors,
-                                 min_fe, a.max_frames, device=device, launcher=launcher)
+                                 min_fe, a.max_frames, device=device, launcher=launcher, first_round=a.first_round)
         dt = time.perf_counter() - t0
         if rank == 0:
             line = res.log_line(a.alist, extra)
@@ -134,7 +146,10 @@ def main(argv=None) -> int:
                 c = res.counts
                 print(json.dumps({"ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "seconds": dt,
                                   "mbit_s": c["frames"] * g.N / dt / 1e6 if dt > 0 else None,
-                                  "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"])}),
+                                  "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
+                                  "precision": a.precision, "schedule": a.schedule, "variant": a.variant,
+                                  "kernel": ctx.kernel_info(cfg)["kernel"], "rounds": res.rounds,
+                                  "frames_decoded": res.frames_decoded}),
                       flush=True)
     if world > 1:
         import torch.distributed as dist
@@ -155,7 +170,7 @@ def _ems_sweep(a, seed, world, rank, device) -> int:
         t0 = time.perf_counter()
         res = sim.simulate_point(run_batch, bits, a.iterations, snr, a.batch, a.min_bit_errors,
                                  a.min_frame_errors if a.min_frame_errors is not None else 40, a.max_frames,
-                                 device=device, iters_in_frames=True)
+                                 device=device, iters_in_frames=True, first_round=a.first_round)
         dt = time.perf_counter() - t0
         if rank == 0:
             line = res.log_line(a.alist, [float(a.nm), a.offset])
@@ -167,7 +182,8 @@ def _ems_sweep(a, seed, world, rank, device) -> int:
                 c = res.counts
                 print(json.dumps({"ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "avg_iters": res.avg_iters,
                                   "seconds": dt, "mbit_s": c["frames"] * bits / dt / 1e6 if dt > 0 else None,
-                                  "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"])}),
+                                  "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
+                                  "precision": "f32", "rounds": res.rounds, "frames_decoded": res.frames_decoded}),
                       flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -1,0 +1,17 @@
+#!/usr/bin/env python3
+"""Summarise LDPC_STAMPS dumps of the ping-pong kernel (rows_pp.hip, -DLDPC_STAMPS):
+per role, s_memtime cycles per barrier interval spent working and waiting.
+usage: pp_stamps.py DUMP INTERVALS_PER_BLOCK"""
+import sys
+import numpy as np
+
+a = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 8192 * 4)
+iv = float(sys.argv[2])
+for i, l in enumerate(a):
+    s = l[: 256 * 16 * 2].reshape(256, 16, 2).astype(np.float64)
+    used = s[s[:, :, 0].sum(axis=1) > 0]
+    for name, w in (("check", slice(0, 8)), ("bit", slice(8, 16))):
+        work = used[:, w, 0] / iv
+        wait = used[:, w, 1] / iv
+        print(f"launch {i} {name:5s}: blocks={len(used)} work {work.mean():7.1f} (min {work.min():7.1f} max "
+              f"{work.max():7.1f})  wait {wait.mean():7.1f}  cycles/interval")

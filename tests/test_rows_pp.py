@@ -1,0 +1,108 @@
+"""The ping-pong fp64 row kernel (ldpcsimulation_amd/csrc/rows_pp.hip): two codewords
+per 1024-thread block, check waves and bit waves overlapped, one barrier interval
+per codeword-iteration.
+
+Its arithmetic is k_rows_fast's (fast64.h), so every output must equal the
+one-codeword-per-block kernel's and the fp64 oracle's (decodeMinSum.cpp:247-263,
+410-515): decisions, per-frame results and counters, for every variant, odd
+batches (the last pair's second slot empty), T = 0 and 1, and frames that break
+the fast premise -- those are re-decoded exactly, one codeword at a time, and the
+other codeword of their pair is unaffected.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import code_path
+from oracle import oracle as O
+
+CODE = "80211n_1944_r12.alist"
+
+
+def _kernel(monkeypatch, name):
+    monkeypatch.setenv("LDPC_ROWS", name)
+
+
+@pytest.mark.gpu
+def test_pp_kernel_selected_for_the_bench_code(gpu_ctx_factory, monkeypatch):
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(CODE)
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50, precision=native.F64)
+    _kernel(monkeypatch, "pp")
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
+    _kernel(monkeypatch, "fast")
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
+    monkeypatch.delenv("LDPC_ROWS")
+    # PEG 504x1008 has M <= 512: one row per thread, the one-codeword kernel
+    assert gpu_ctx_factory("PEGReg504x1008.alist").kernel_info(cfg)["kernel"] == "rows_fast"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,T,v", [
+    (2048, 50, dict(variant=1, alpha=1.25)),     # the bench configuration
+    (1001, 50, dict(variant=0)),                 # odd batch: the last pair has one codeword
+    (257, 7, dict(variant=2, delta=0.15)),
+    (64, 1, dict(variant=1, alpha=1.1)),         # IEEE division (alpha not P*2^E)
+    (3, 0, dict(variant=1, alpha=1.25)),         # no iteration: decisions of the channel
+    (1, 13, dict(variant=0)),                    # one codeword, empty partner slot
+])
+def test_pp_equals_rows_fast_and_oracle(gpu_ctx_factory, monkeypatch, batch, T, v):
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(CODE)
+    cfg = native.DecoderConfig(T=T, precision=native.F64, **v)
+    _kernel(monkeypatch, "fast")
+    y0, d0, f0, c0 = ctx.sim_trace(1.5, 0.5, cfg, seed=77, stream_id=5, first_cw=123, batch=batch)
+    _kernel(monkeypatch, "pp")
+    y1, d1, f1, c1 = ctx.sim_trace(1.5, 0.5, cfg, seed=77, stream_id=5, first_cw=123, batch=batch)
+    assert ctx.redo_count() == 0
+    assert np.array_equal(y0, y1)
+    assert np.array_equal(d0, d1)
+    assert np.array_equal(f0, f1)
+    assert c0.as_dict() == c1.as_dict()
+    n = min(batch, 256)
+    want = O.Alist(code_path(CODE)).decode(y1[:n], T, O.Cfg(**v), workers=16)
+    assert int((d1[:n] != want).sum()) == 0
+    assert np.array_equal(f1["bit_err"][:n], (want != 1).sum(axis=1))
+
+
+def _glibc_frames(N, nframes, ebn0, R, seed):
+    g = O.GlibcRandom(seed)
+    sigma = math.sqrt(10 ** (-ebn0 / 10) / R / 2)
+    c = np.ones(N, dtype=np.int32)
+    return np.stack([g.channel(c, sigma) for _ in range(nframes)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0)),
+                                     ("oms", dict(variant=2, delta=0.15))])
+def test_pp_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, vname, v):
+    """Frames 1-5 break the fast premise (|y| >= 2^1000, tiny minima, inf, NaN, growth
+    past 2^1000); their pair partners (0, and the unbroken frames 6-9 sharing no pair
+    with them) decode normally. Everything equals the fp64 oracle; the re-decode list
+    holds the broken codewords only (not whole pairs)."""
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(CODE)
+    _kernel(monkeypatch, "pp")
+    N = ctx.graph.N
+    y = _glibc_frames(N, 12, 1.5, 0.5, seed=4244)
+    y[1] *= 1e305
+    y[2] *= 1e-305
+    y[3, 5] = np.inf
+    y[4, 7] = np.nan
+    y[5] *= 2.0 ** 995
+    y[6, ::3] = -0.0
+    y[7] = np.where(np.arange(N) % 2 == 0, 0.5, -1.0)
+    A = O.Alist(code_path(CODE))
+    for T in (1, 7, 30):
+        cfg = native.DecoderConfig(T=T, precision=native.F64, **v)
+        assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
+        d, fr, cnt = ctx.decode(y, cfg)
+        redo = ctx.redo_count()
+        want = A.decode(y, T, O.Cfg(**v), workers=8)
+        mism = (d != want).sum(axis=1)
+        assert int(mism.sum()) == 0, f"T={T}: mismatching frames {np.nonzero(mism)[0].tolist()}"
+        w = (want != 1).sum(axis=1)
+        assert np.array_equal(fr["bit_err"], w)
+        assert cnt.frames == len(y) and cnt.bit_err == int(w.sum()) and cnt.iters == T * len(y)
+        assert 3 <= redo <= 5, redo      # frames 1, 3, 4 always; 2 (fast division) and 5 (growth) may

@@ -83,15 +83,31 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, batch, q):
+def _worker(rank, world, port, batch, q, first_round=None, high_fer=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        res = sim.simulate_point(fake_frames, N, T, 1.5, batch)
-        q.put((rank, res.counts, res.hist.tolist(), res.rounds))
+        res = sim.simulate_point(fake_frames_high_fer if high_fer else fake_frames, N, T, 1.0, batch,
+                                 first_round=first_round)
+        q.put((rank, res.counts, res.hist.tolist(), res.rounds, res.frames_decoded))
     finally:
         dist.destroy_process_group()
+
+
+def _two_ranks(batch, first_round=None, high_fer=False):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, batch, q, first_round, high_fer)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
 
 
 @pytest.mark.parametrize("batch", [16, 300])
@@ -108,9 +124,71 @@ def test_two_ranks_gloo_identical_to_sequential(batch):
         p.join(timeout=60)
         assert p.exitcode == 0
     want, hist = sequential()
-    for rank, counts, h, rounds in out:
+    for rank, counts, h, rounds, _ in out:
         assert counts == want, rank
         assert np.array_equal(np.array(h), hist)
+
+
+def fake_frames_high_fer(first, n):
+    """A low-SNR point (FER ~0.4, as 802.11n N=1944 NMS at 1.0 dB): the stop rule is
+    reached after ~100 frames."""
+    out = fake_frames(first, n)
+    f = np.arange(first, first + n, dtype=np.int64)
+    h = (f * 2246822519) & 0xFFFFFFFF
+    out["bit_err"] = np.where((h >> 9) % 5 < 2, (h % 37) + 3, 0)
+    return out
+
+
+def sequential_of(gen, min_bit=200, min_frame=40):
+    acc = np.zeros(6, dtype=np.int64)
+    f = 0
+    while acc[0] < min_bit or acc[1] < min_frame:
+        r = gen(f, 1)[0]
+        w = int(r["bit_err"])
+        acc += (w, w > 0, r["uncoded_bit_err"], 1, T, r["syndrome_fail"])
+        f += 1
+    return dict(zip(sim.COUNT_KEYS, (int(x) for x in acc)))
+
+
+def test_round_sizes_double_up_to_batch():
+    g = sim.round_sizes(65536)
+    assert [next(g) for _ in range(9)] == [1024, 2048, 4096, 8192, 16384, 32768, 65536, 65536, 65536]
+    g = sim.round_sizes(3000, first_round=1000)
+    assert [next(g) for _ in range(4)] == [1000, 2000, 3000, 3000]
+    g = sim.round_sizes(500)
+    assert [next(g) for _ in range(2)] == [500, 500]
+
+
+@pytest.mark.parametrize("first_round", [None, 1, 100, 65536])
+def test_adaptive_rounds_same_totals(first_round):
+    """Any first-round size gives the sequential totals and histogram (exact_stop)."""
+    want, hist = sequential()
+    res = sim.simulate_point(fake_frames, N, T, 1.5, 65536, first_round=first_round)
+    assert res.counts == want and np.array_equal(res.hist, hist)
+    L = _FakeLauncher()
+    res = sim.simulate_point(fake_frames, N, T, 1.5, 65536, first_round=first_round, launcher=L)
+    assert res.counts == want and np.array_equal(res.hist, hist) and not L.pending
+
+
+def test_adaptive_rounds_decode_fewer_frames_at_high_fer():
+    """at FER ~0.4 the default first round (1024) stops after one
+    round, where fixed 65,536-frame rounds decode 65,536 frames for ~100 needed."""
+    want = sequential_of(fake_frames_high_fer)
+    assert want["frames"] < 200
+    fixed = sim.simulate_point(fake_frames_high_fer, N, T, 1.0, 65536, first_round=65536)
+    adapt = sim.simulate_point(fake_frames_high_fer, N, T, 1.0, 65536)
+    assert fixed.counts == want and adapt.counts == want
+    assert fixed.frames_decoded == 65536 and adapt.frames_decoded == 1024
+
+
+def test_adaptive_rounds_two_ranks_gloo():
+    """world 2 (gloo): the adaptive rounds give the sequential totals on both ranks and
+    decode 2 x 1024 frames at the high-FER point (fixed rounds: 2 x 65,536)."""
+    want = sequential_of(fake_frames_high_fer)
+    for first_round, decoded in ((None, 2048), (65536, 131072)):
+        for rank, counts, h, rounds, dec in _two_ranks(65536, first_round, high_fer=True):
+            assert counts == want, (rank, first_round)
+            assert dec == decoded, (rank, first_round, dec)
 
 
 def fake_frames_early_stop(first, n):
