@@ -27,12 +27,16 @@ $(BINDIR):
 # -load-store-opt: keep the bit-phase LDS reads as single ds_read_b64 (2 LDS
 # cycles each) instead of merged ds_read2st64_b64 (8 cycles for the same data).
 KERNFLAGS = -Xclang -target-feature -Xclang -load-store-opt
+# Loop headers on 32-byte boundaries: without it the ping-pong kernel's time moved
+# by up to 4 % with the code layout (s_nop shifts at the kernel entry: 14.85-15.47
+# ms); aligned, 14.78-14.85 ms for every shift.
+ALIGNFLAGS = -falign-loops=32
 $(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/rows_fast.o: $(CSRC)/rows_fast.hip $(CSRC)/fast64.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/rows_pp.o: $(CSRC)/rows_pp.hip $(CSRC)/fast64.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/bp.o: $(CSRC)/bp.hip $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
@@ -103,9 +107,17 @@ fastvariant: $(OBJS)
 # Ping-pong kernel A/B variants: make ppvariant NAME=x VFLAGS="-DLDPC_PP_..." -> lib/variants/libldpc_hip_x.so
 ppvariant: $(OBJS)
 	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o $(CSRC)/rows_pp.hip
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o $(CSRC)/rows_pp.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/rows_pp.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o
+
+# EMS kernel A/B variants: make nbvariant NAME=x VFLAGS="-DLDPC_EMS_..." [NBSRC=file] -> lib/variants/libldpc_hip_x.so
+NBSRC ?= $(CSRC)/nb.hip
+nbvariant: $(OBJS)
+	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/nb.o $(NBSRC)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/nb.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/nb.o
 
 # GDBF kernel A/B variants: make gdbfvariant NAME=x VFLAGS="-DLDPC_GDBF_..." -> lib/variants/libldpc_hip_x.so
 gdbfvariant: $(OBJS)
@@ -131,7 +143,7 @@ ref:
 clean:
 	rm -rf $(LIBDIR) $(BINDIR) oracle/liboracle.so
 
-.PHONY: all oracle ref clean variant fastvariant ppvariant
+.PHONY: all oracle ref clean variant fastvariant ppvariant nbvariant
 
 # Host-code sanitizer build: graph.cpp (the Tanner-graph compiler)
 # and the CPU oracle under AddressSanitizer + UBSan, driven over code files.

@@ -95,14 +95,24 @@ def parse(argv=None):
 
 
 def cpu_share() -> int:
-    """Cores this process may use: its CPU affinity, capped by the box's share
-    (OMP_NUM_THREADS, 16 on the GPU box whose affinity shows the whole host)."""
+    """Cores this process may use: its CPU affinity, capped by OMP_NUM_THREADS when
+    that is set (the GPU box sets it to its per-GPU share, 16, while its affinity
+    shows the whole host)."""
     try:
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = os.cpu_count() or 1
-    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    cap = int(env) if env.strip().isdigit() and int(env) > 0 else aff
     return max(1, min(aff, cap))
+
+
+def host_cores() -> int:
+    """All cores this process's affinity shows (the whole host on the GPU box)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
 def _final(out: str):
@@ -159,8 +169,12 @@ def cpu_baseline(alist: str, T: int, alpha: float, ebn0: float, procs: int) -> d
                                  env=dict(os.environ, REF_SEED="7"), capture_output=True, text=True, check=True).stdout
             single_g = _final(out)[0] * N / (time.perf_counter() - ts) / 1e6
     rates = [f * N / w / 1e6 for f, w in zip(frames, walls)]
+    hc = host_cores()
     return {"value": float(sum(rates)), "unit": "Mbit/s", "cores": procs, "kind": "reference",
             "single_core_mbit_s": float(np.median(rates)),
+            # the whole host is not run here (the box allots its GPU a 16-core share): the
+            # full-host aggregate is the measured per-core rate times the host's cores
+            "host_cores": hc, "host_aggregate_mbit_s_extrapolated": float(np.median(rates)) * hc,
             "single_core_mbit_s_as_shipped_O0_g": single_g,
             "cpu_model": _cpu_model(),
             "frames_per_process_min": int(min(frames)), "frames_total": int(sum(frames)),
@@ -339,13 +353,16 @@ def main():
     if rank == 0:
         tot = head["tot"]
         rl = roofline(head)
-        traffic, traffic_src = None, None
+        traffic, traffic_src, traffic_kernel = None, None, None
         try:
             tj = json.load(open(args.traffic_json))
             tj = tj.get(args.precision, {})
-            traffic, traffic_src = tj.get("hbm_bytes_per_launch"), tj.get("source")
+            traffic, traffic_src, traffic_kernel = tj.get("hbm_bytes_per_launch"), tj.get("source"), tj.get("kernel")
         except (OSError, ValueError):
             pass
+        # the PMC bytes (a separate rocprofv3 --pmc pass of this same command, scripts/profile_round.sh)
+        # over this run's live average launch time, against the HBM peak
+        traffic_gbs = traffic / (rl["avg_kernel_ms"] / 1e3) / 1e9 if traffic else None
         k_fe, n_fe = int(tot[1]), int(tot[3])
         from ldpcsimulation_amd.sim import two_proportion_z, wilson_interval
         fer = {"ebn0_db": args.ebn0, "frame_err": k_fe, "frames": n_fe, "fer": k_fe / n_fe,
@@ -368,7 +385,10 @@ def main():
                        "global_batch": B * world, "T": args.T, "ebn0_db": args.ebn0, "variant": "nms",
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": {**{k: rl.get(k) for k in ("bound", "achieved", "peak", "unit", "frac")},
-                         "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC)",
+                         "traffic_gbs": traffic_gbs,
+                         "traffic_frac_of_hbm_peak": traffic_gbs / (HBM_PEAK / 1e9) if traffic_gbs else None,
+                         "traffic_source": traffic_src, "traffic_kernel": traffic_kernel,
                          **{k: v for k, v in rl.items() if k not in ("bound", "achieved", "peak", "unit", "frac")}},
             "fer": fer,
             "kernel_info": ctx.kernel_info(head["cfg"]),

@@ -125,6 +125,11 @@ typedef struct {
 
 int         ldpc_abi_version(void);
 const char *ldpc_last_error(void);
+/* 1 when the fp64 NMS division m / alpha (applyNormalization,
+ * decodeMinSum.cpp:494-499) runs as Markstein's q = m*r, q += fma(-q, alpha, m)*r
+ * with r = RN(1/alpha) -- exact for alpha = P * 2^E, odd P < 2^20, 2^-900 < alpha
+ * <= 2^60 -- else 0 (IEEE division). No device call. */
+int         ldpc_f64_nms_fast_division(double alpha);
 
 /* ---- graph (H matrix) ------------------------------------------------ */
 /* Arrays exactly as alist_struct (inc/alist.h:21-36): nlist[i] has

@@ -78,6 +78,7 @@ struct ldpc_ctx {
     DevBuf graph, counts, hist, y_stage, c_stage, d_stage, fw_stage, cw_table, gscratch, p_stage;
     int cw_rows = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    ldpc::AuxStream aux;          // second stream of the flooding phase launches (kernels.h)
     bool timed = false;
     char force[16] = {0};        // LDPC_KERNEL=lds|flood|global (LDPC_FORCE_GLOBAL=1 = global), tests only
     bool has_rs = false;
@@ -137,6 +138,7 @@ static hipError_t upload_row_sched(const ldpc::RowSchedule &hs, DevBuf &buf, ldp
 extern "C" {
 
 int ldpc_abi_version(void) { return LDPC_ABI_VERSION; }
+int ldpc_f64_nms_fast_division(double alpha) { return ldpc::markstein_exact_alpha(alpha) ? 1 : 0; }
 const char *ldpc_last_error(void) { return g_last_error.c_str(); }
 
 // ----------------------------------------------------------------- graph
@@ -244,6 +246,9 @@ static void ctx_free(ldpc_ctx *c)
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->aux.fork) (void)hipEventDestroy(c->aux.fork);
+    if (c->aux.join) (void)hipEventDestroy(c->aux.join);
+    if (c->aux.s) (void)hipStreamDestroy(c->aux.s);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -288,6 +293,9 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
     c->stream = c->own;
     CTX_TRY(hipEventCreate(&c->ev0));
     CTX_TRY(hipEventCreate(&c->ev1));
+    CTX_TRY(hipStreamCreateWithFlags(&c->aux.s, hipStreamNonBlocking));
+    CTX_TRY(hipEventCreateWithFlags(&c->aux.fork, hipEventDisableTiming));
+    CTX_TRY(hipEventCreateWithFlags(&c->aux.join, hipEventDisableTiming));
 
     // Graph upload: one allocation, 256-B aligned sections.
     const int dcs = g->maxdc > 0 ? g->maxdc : 1;
@@ -530,13 +538,14 @@ static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool 
            ldpc::redo_lds_bytes(c->dg, f64) <= 160 * 1024;
 }
 
-// fp64 on the fast path: the ping-pong kernel (two codewords per block, check
-// and bit waves overlapped) when the schedule fits it; LDPC_ROWS=fast keeps
-// the one-codeword-per-block k_rows_fast. Opt-in (LDPC_ROWS=pp) until measured.
+// fp64 on the fast path: the ping-pong kernel (rows_pp.hip: two codewords per
+// 1024-thread block, check and bit waves overlapped; 14.8 vs 16.2 ms per bench
+// launch) when the row schedule fits it; LDPC_ROWS=fast keeps the one-codeword-
+// per-block k_rows_fast (and LDPC_ROWS=old the row kernel).
 static bool use_rows_pp(const ldpc_ctx *c, bool f64)
 {
     const char *env = std::getenv("LDPC_ROWS");
-    if (!f64 || !(env && std::strcmp(env, "pp") == 0)) return false;
+    if (!f64 || (env && std::strcmp(env, "fast") == 0)) return false;
     return ldpc::rows_pp_supported(c->dg, c->rs);
 }
 
@@ -613,7 +622,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
     } else if (layered) {
         HIP_TRY(ldpc::launch_layered(c->dg, a, f64, kc, c->fs, c->ls, c->gscratch.p, gblocks, c->stream));
     } else if (kc.name[0] == 'f' && use_flood_phase())
-        HIP_TRY(ldpc::launch_flood_phase(c->dg, c->fs, a, f64, kc, c->gscratch.p, c->gscratch.n, c->stream));
+        HIP_TRY(ldpc::launch_flood_phase(c->dg, c->fs, a, f64, kc, c->gscratch.p, c->gscratch.n, c->stream, &c->aux));
     else
         HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream,
                                     c->has_rs ? &c->rs : nullptr, c->num_cus, c->has_fs ? &c->fs : nullptr));
@@ -639,6 +648,10 @@ static int read_counts(ldpc_ctx *c, ldpc_counts *out, int reset)
     unsigned long long h[8];
     HIP_TRY(hipMemcpyAsync(h, c->counts.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (h[7]) {   // a kernel's in-block synchronisation gave up (rows_pp.hip pp_wait): results invalid
+        (void)hipMemsetAsync(c->counts.p, 0, c->counts.n, c->stream);
+        return set_err(LDPC_ERR_DEVICE, "%llu workgroup(s) timed out in the dataflow sync; counts discarded", h[7]);
+    }
     if (out) {
         out->bit_err = (int64_t)h[0];
         out->frame_err = (int64_t)h[1];

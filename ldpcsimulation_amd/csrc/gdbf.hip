@@ -207,7 +207,8 @@ __device__ __forceinline__ void gdbf_codeword(const GdbfArgs &a, const DevGraph 
                                   (a.stream_id & 0xFFFFFu) | ((uint32_t)(it + 1) << 20), k0, k1, u);
                     if (qprob) {
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) pv[q] = ((F)u[q] + F(0.5)) * (F)0x1p-32;   // in (0, 1)
+                        for (int q = 0; q < 4; ++q)   // in (0, 1): fp32 from the top 24 bits ((float)u rounds up to 2^32)
+                            pv[q] = sizeof(F) == 8 ? ((F)u[q] + F(0.5)) * (F)0x1p-32 : ((F)(u[q] >> 8) + F(0.5)) * (F)0x1p-24;
                     } else {
                         float n[4];
                         pert_normals(u[0], u[1], n[0], n[1]);

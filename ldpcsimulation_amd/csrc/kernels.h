@@ -91,8 +91,16 @@ hipError_t launch_decode(const DevGraph &g, const DecodeArgs &a, bool f64, const
 int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc);
 // Flooding of codes beyond LDS as one launch per phase over an Infinity-Cache-
 // resident set of codewords (kernels.hip k_flood_*); gscratch as for "flood".
+// aux (may be null): a second stream with fork/join events; the resident set is
+// then split in two halves, one per stream, so one half's launch boundaries
+// overlap the other half's kernels.
+struct AuxStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
 hipError_t launch_flood_phase(const DevGraph &g, const FloodSched &fs, const DecodeArgs &a, bool f64,
-                              const KernelChoice &kc, void *gscratch, size_t gscratch_bytes, hipStream_t s);
+                              const KernelChoice &kc, void *gscratch, size_t gscratch_bytes, hipStream_t s,
+                              const AuxStream *aux = nullptr);
 
 // Layered schedule (k_decode_layered_*): state in LDS when it fits
 // ("layered_lds"), else in a global slot per block ("layered_global").

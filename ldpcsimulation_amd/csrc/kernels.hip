@@ -750,57 +750,127 @@ static int flood_phase_resident(size_t slot_bytes, size_t gscratch_bytes)
     return k < 1 ? 1 : (int)k;
 }
 
+// The phase launches of resident slots [lo, lo + n) of a chunk whose first codeword
+// is b0: init, T x (check, bit), finish, accounting -- issued on stream s.
+template <typename F, int SRC>
+struct FloodHalf {
+    const DevGraph *g;
+    const FloodSched *fs;
+    const DecodeArgs *a;
+    unsigned char *scratch;
+    size_t sb;
+    int *unc, *wsum, *ssum;   // per-slot counters (index = slot)
+    hipStream_t s;
+    int lo, n;
+    hipError_t begin(int b0) const
+    {
+        if (n <= 0) return hipSuccess;
+        hipError_t e = hipMemsetAsync(unc + lo, 0, sizeof(int) * (size_t)n, s);
+        if (e == hipSuccess) e = hipMemsetAsync(wsum + lo, 0, sizeof(int) * (size_t)n, s);
+        if (e == hipSuccess) e = hipMemsetAsync(ssum + lo, 0, sizeof(int) * (size_t)n, s);
+        if (e != hipSuccess) return e;
+        const int ib = ((g->N + 3) / 4 + 255) / 256;
+        hipLaunchKernelGGL((k_flood_init<F, SRC>), dim3(ib > 1 ? ib : 1, n), dim3(256), 0, s, *a, *g, *fs,
+                           scratch + sb * (size_t)lo, sb, b0 + lo, unc + lo);
+        return hipSuccess;
+    }
+    void check() const
+    {
+        if (n <= 0) return;
+        const int NPc = fs->M_pad;
+#if LDPC_FLOOD_XCD
+        const dim3 cg(8 * ((NPc + 255) / 256));
+#else
+        const dim3 cg((NPc + 255) / 256, (n + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW);
+#endif
+        unsigned char *sc = scratch + sb * (size_t)lo;
+        if (fs->dc <= 8)
+            hipLaunchKernelGGL((k_flood_check<F, 8>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n);
+        else if (fs->dc <= 16)
+            hipLaunchKernelGGL((k_flood_check<F, 16>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n);
+        else
+            hipLaunchKernelGGL((k_flood_check<F, 32>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n);
+    }
+    void bit() const
+    {
+        if (n <= 0) return;
+        const int NP = fs->ngroups * 64;
+#if LDPC_FLOOD_XCD
+        const dim3 bg(8 * ((NP + 255) / 256));
+#else
+        const dim3 bg((NP + 255) / 256, (n + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW);
+#endif
+        hipLaunchKernelGGL((k_flood_bit<F>), bg, dim3(256), 0, s, *fs, scratch + sb * (size_t)lo, sb, n);
+    }
+    void end(int b0) const
+    {
+        if (n <= 0) return;
+        const int gy = (n + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW;
+        const int fx = ((g->N > fs->M_pad ? g->N : fs->M_pad) + 255) / 256;
+        hipLaunchKernelGGL((k_flood_finish<F>), dim3(fx, gy), dim3(256), 0, s, *a, *g, *fs, scratch + sb * (size_t)lo,
+                           sb, b0 + lo, n, wsum + lo, ssum + lo);
+        hipLaunchKernelGGL(k_flood_account, dim3((n + 255) / 256), dim3(256), 0, s, *a, b0 + lo, n, unc + lo, wsum + lo,
+                           ssum + lo);
+    }
+};
+
+// LDPC_FLOOD_STREAMS=2: the resident set in two halves on two streams (aux).
+static bool flood_two_streams()
+{
+    const char *e = std::getenv("LDPC_FLOOD_STREAMS");
+    return e && std::atoi(e) == 2;
+}
+
 template <typename F, int SRC>
 static hipError_t launch_flood_phase_t(const DevGraph &g, const FloodSched &fs, const DecodeArgs &a,
-                                       const KernelChoice &kc, void *gs, size_t gs_bytes, hipStream_t s)
+                                       const KernelChoice &kc, void *gs, size_t gs_bytes, hipStream_t s,
+                                       const AuxStream *aux)
 {
     const size_t sb = kc.scratch_per_block;
     const int K = flood_phase_resident(sb, gs_bytes);
     unsigned char *scratch = (unsigned char *)gs;
     int *unc = reinterpret_cast<int *>(scratch + sb * (size_t)K);   // per-slot counters after the slots
     int *wsum = unc + K, *ssum = wsum + K;
-    const int NP = fs.ngroups * 64;
+    const bool two = aux && aux->s && flood_two_streams() && K >= 2;
+    hipError_t e;
+    if (two) {   // fork: the aux stream starts after everything queued on s
+        if ((e = hipEventRecord(aux->fork, s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(aux->s, aux->fork, 0)) != hipSuccess) return e;
+    }
     for (int b0 = 0; b0 < a.batch; b0 += K) {
         const int nres = a.batch - b0 < K ? a.batch - b0 : K;
-        hipError_t e = hipMemsetAsync(unc, 0, sizeof(int) * 3 * (size_t)K, s);
-        if (e != hipSuccess) return e;
-        const int ib = ((g.N + 3) / 4 + 255) / 256;
-        hipLaunchKernelGGL((k_flood_init<F, SRC>), dim3(ib > 1 ? ib : 1, nres), dim3(256), 0, s, a, g, fs, scratch, sb,
-                           b0, unc);
-        const int gy = (nres + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW;
-#if LDPC_FLOOD_XCD
-        const dim3 cg(8 * ((fs.M_pad + 255) / 256)), bg(8 * ((NP + 255) / 256));
-#else
-        const dim3 cg((fs.M_pad + 255) / 256, gy), bg((NP + 255) / 256, gy);
-#endif
+        const int na = two ? (nres + 1) / 2 : nres;
+        const FloodHalf<F, SRC> A{&g, &fs, &a, scratch, sb, unc, wsum, ssum, s, 0, na};
+        const FloodHalf<F, SRC> B{&g, &fs, &a, scratch, sb, unc, wsum, ssum, two ? aux->s : s, na, nres - na};
+        if ((e = A.begin(b0)) != hipSuccess) return e;
+        if ((e = B.begin(b0)) != hipSuccess) return e;
         for (int it = 0; it < a.T; ++it) {
-            if (fs.dc <= 8)
-                hipLaunchKernelGGL((k_flood_check<F, 8>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
-            else if (fs.dc <= 16)
-                hipLaunchKernelGGL((k_flood_check<F, 16>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
-            else
-                hipLaunchKernelGGL((k_flood_check<F, 32>), cg, dim3(256), 0, s, a, fs, scratch, sb, nres);
-            hipLaunchKernelGGL((k_flood_bit<F>), bg, dim3(256), 0, s, fs, scratch, sb, nres);
+            A.check();
+            B.check();
+            A.bit();
+            B.bit();
         }
-        const int fx = ((g.N > fs.M_pad ? g.N : fs.M_pad) + 255) / 256;
-        hipLaunchKernelGGL((k_flood_finish<F>), dim3(fx, gy), dim3(256), 0, s, a, g, fs, scratch, sb, b0, nres, wsum,
-                           ssum);
-        hipLaunchKernelGGL(k_flood_account, dim3((nres + 255) / 256), dim3(256), 0, s, a, b0, nres, unc, wsum, ssum);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
+        A.end(b0);
+        B.end(b0);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (two) {   // join: s continues after the aux stream's last launch
+        if ((e = hipEventRecord(aux->join, aux->s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, aux->join, 0)) != hipSuccess) return e;
     }
     return hipSuccess;
 }
 
 hipError_t launch_flood_phase(const DevGraph &g, const FloodSched &fs, const DecodeArgs &a, bool f64,
-                              const KernelChoice &kc, void *gscratch, size_t gscratch_bytes, hipStream_t s)
+                              const KernelChoice &kc, void *gscratch, size_t gscratch_bytes, hipStream_t s,
+                              const AuxStream *aux)
 {
     if (a.batch <= 0) return hipSuccess;
     if (f64)
-        return a.src == SRC_GIVEN ? launch_flood_phase_t<double, SRC_GIVEN>(g, fs, a, kc, gscratch, gscratch_bytes, s)
-                                  : launch_flood_phase_t<double, SRC_PHILOX>(g, fs, a, kc, gscratch, gscratch_bytes, s);
-    return a.src == SRC_GIVEN ? launch_flood_phase_t<float, SRC_GIVEN>(g, fs, a, kc, gscratch, gscratch_bytes, s)
-                              : launch_flood_phase_t<float, SRC_PHILOX>(g, fs, a, kc, gscratch, gscratch_bytes, s);
+        return a.src == SRC_GIVEN ? launch_flood_phase_t<double, SRC_GIVEN>(g, fs, a, kc, gscratch, gscratch_bytes, s, aux)
+                                  : launch_flood_phase_t<double, SRC_PHILOX>(g, fs, a, kc, gscratch, gscratch_bytes, s, aux);
+    return a.src == SRC_GIVEN ? launch_flood_phase_t<float, SRC_GIVEN>(g, fs, a, kc, gscratch, gscratch_bytes, s, aux)
+                              : launch_flood_phase_t<float, SRC_PHILOX>(g, fs, a, kc, gscratch, gscratch_bytes, s, aux);
 }
 
 // =====================================================================

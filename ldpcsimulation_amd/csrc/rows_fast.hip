@@ -89,7 +89,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
     const int N = g.N, EA = rs.e_pad + 64;
     P *app = reinterpret_cast<P *>(smem);          // [N + 2]: bit N is the +INF sentinel of padding edges
     P *c2v = app + (N + 2);                        // [EA] bit-slot-major; last 64: per-lane dummies
-    int *red = reinterpret_cast<int *>(c2v + EA);  // [31]: premise flag of the current group; [32, 80): sums; [96, 108): acc
+    int *red = reinterpret_cast<int *>(c2v + EA);  // [31]: premise flag; [32, 128): block sums (16 waves x 6); [128, 140): acc
     const uint32_t app_base = lds_addr_of(app), c2v_base = lds_addr_of(c2v);   // LDS byte addresses
 
     int deg[RPT];
@@ -129,7 +129,10 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
     const int ngrp = (a.batch + C - 1) / C;
     // the block's totals (thread 0), added to a.counts once at the end; in the
     // dynamic area (no static LDS: app starts at LDS address 0)
-    unsigned long long *acc = reinterpret_cast<unsigned long long *>(red + 96);
+    // past block_sum_n's area at every block size (16 waves x 3C sums; ADVICE r2: red + 96 was
+    // overwritten by waves 10-12 of a 1024-thread fp32 pair block)
+    static_assert(32 + 16 * 3 * C <= 128, "block sums overlap the accumulators");
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(red + 128);
     if (tid == 0)
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
@@ -143,7 +146,10 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             unc[c] = 0;
             cvec[c] = nullptr;
             const int b = grp * C + c;
-            if (b >= a.batch) continue;
+            if (b >= a.batch) {   // missing partner of an odd batch: benign +1 samples, never a premise break
+                for (int v = tid; v < N; v += nt) c2v[v].v[c] = F(1);
+                continue;
+            }
             const uint64_t cw = a.first_cw + (uint64_t)b;
             if (SRC == SRC_GIVEN) {
                 if (a.c) cvec[c] = a.c + (size_t)b * N;
@@ -345,7 +351,9 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
 // Markstein's correction is then exact (header).
 bool markstein_exact_alpha(double alpha)
 {
-    if (!(alpha > 0x1p-900) || !(alpha < 0x1p900)) return false;
+    // |alpha| <= 2^60: a minimum >= 2^-960 then divides to >= 2^-1020, a normal
+    // quotient, where the 1/(2P)-ulp midpoint argument holds
+    if (!(alpha > 0x1p-900) || !(alpha <= 0x1p60)) return false;
     unsigned long long b;
     __builtin_memcpy(&b, &alpha, 8);
     const unsigned long long sig = (b & ((1ull << 52) - 1)) | (1ull << 52);   // 53-bit significand

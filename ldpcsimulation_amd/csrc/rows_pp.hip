@@ -24,9 +24,8 @@
 // in nlist order), hence the decisions equal the reference's bit for bit.
 //
 // The c2v a row sent last iteration (the `- msg` of :469) is kept per slot in
-// registers (prev, 2 slots x 2 rows x 8 edges) or, with PREV_LDS, re-read from
-// the row's own c2v slots (8 more ds_read_b64 per row, 32 fewer VGPRs... the
-// default is the measured winner).
+// registers (prev: 2 slots x rows x 8 edges); re-reading it from the row's own
+// c2v slots instead (8 more ds_read_b64 per row) measured slower (16.9 vs 14.7 ms).
 //
 // Premise failures (fast64.h): the slot's flag is raised and the codeword is
 // re-decoded on the exact path (k_redo) after the launch; the other slot of
@@ -50,12 +49,18 @@ namespace {
 
 // Timing experiments only (wrong results; `make ppvariant`): LDPC_PP_EXP =
 // 1 bit role idle (barriers only), 2 check role idle, 3 check node replaced by
-// a subtraction, 4 no c2v scatters.
+// a subtraction, 4 no c2v scatters, 5 gathers at lane-contiguous addresses (no
+// bank conflicts), 6 scatters at lane-contiguous addresses, 7 both 5 and 6.
+// LDPC_PP_BITDELAY: s_sleep units (64 cycles) the bit waves wait at an interval's start.
 #ifndef LDPC_PP_EXP
 #define LDPC_PP_EXP 0
 #endif
+#ifndef LDPC_PP_BITDELAY
+#define LDPC_PP_BITDELAY 0
+#endif
 
-// Wave priority (s_setprio): 0 none, 1 check role above the bit role, 2 the reverse.
+// Wave priority (s_setprio): 0 none, 1 check role above the bit role, 2 the reverse,
+// 3 the younger half of each role (waves 4-7, 12-15) above the older half.
 #ifndef LDPC_PP_PRIO
 #define LDPC_PP_PRIO 0
 #endif
@@ -89,7 +94,36 @@ namespace {
 #endif
 
 constexpr int kPPRole = 512;          // threads per role
-constexpr int kPPRedInts = 160;       // [0,2): slot flags; [32,128): block sums; [128,140): acc (6 x u64)
+constexpr int kPPRedInts = 160;       // [0,2): slot flags; [2]: sync abort; [4,8): sync counters;
+                                      // [32,128): block sums; [128,140): acc (6 x u64)
+constexpr int kPPSyncAbort = 2, kPPCheckDone = 4, kPPBitDone = 6;   // red[] indices (counters per slot)
+constexpr unsigned kPPSpinLimit = 1u << 22;   // polls (~64 cycles apart) before a wait gives up
+
+// Dataflow sync (MODE 2): LDS counters instead of block barriers. A wave waits
+// (polling, s_sleep between polls) until counter c reaches `target`, then
+// acquires; the producer side releases (all its LDS writes complete) and adds 1
+// per wave. A wait that never ends (a bug) gives up after kPPSpinLimit polls,
+// raises the abort word -- every other wait of the block then gives up within
+// 256 polls, so the grid drains -- and the host reports it (counts[7],
+// ldpc_ctx_read_counts).
+__device__ __forceinline__ void pp_wait(int *red, int c, int target)
+{
+    unsigned n = 0;
+#pragma nounroll
+    while (__builtin_amdgcn_readfirstlane(__atomic_load_n(&red[c], __ATOMIC_RELAXED)) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++n & 255u) == 0 && (n >= kPPSpinLimit || __atomic_load_n(&red[kPPSyncAbort], __ATOMIC_RELAXED))) {
+            __atomic_store_n(&red[kPPSyncAbort], 1, __ATOMIC_RELAXED);
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void pp_signal(int *red, int c)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __atomic_fetch_add(&red[c], 1, __ATOMIC_RELAXED);
+}
 
 struct PPSlots {
     Pack<double, 1> *app[2], *c2v[2];
@@ -198,135 +232,54 @@ __device__ __forceinline__ void pp_account(const DecodeArgs &a, const PPSlots &s
     }
 }
 
-// ---- the check role: rows t and t + 512 of both slots ----
-template <int SRC, int DC, int VAR, bool FDIV, bool PREV_LDS>
-__device__ __forceinline__ void pp_check_role(const DecodeArgs &a, const DevGraph &g, const RowSched &rs,
-                                              const PPSlots &s, unsigned *redo, unsigned long long *acc)
+// ---- one wave's work: R check rows of each slot and, with HB, CPT bit slots ----
+// Row r of thread t is row-schedule row t + 512 r. The split is per wave (an
+// SGPR branch in the kernel): MODE 0 gives waves 0-7 rows t, t + 512 (R = 2)
+// and waves 8-15 the bit slots of schedule thread t - 512 (HB); MODE 1 gives
+// every thread its row t (R = 1) and waves 8-15 also the bit slots, so the
+// check rows spread over 4 waves per SIMD with one row each.
+template <int SRC, int DC, int CPT, int VAR, bool FDIV, int R, bool HB, bool SYNC>
+__device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, const RowSched &rs, const PPSlots &s,
+                                        unsigned *redo, unsigned long long *acc)
 {
     using P = Pack<double, 1>;
-    constexpr int RPT = 2;
-    const int tid = threadIdx.x, N = g.N;
-    int deg[RPT];
-    uint32_t colw[RPT][DC / 2], posw[RPT][DC / 2];
+    constexpr int RR = R > 0 ? R : 1;   // array extents
+    const int tid = threadIdx.x, N = g.N, lane = tid & 63;
+    // check rows: schedule, and the c2v each sent last iteration, per slot
+    [[maybe_unused]] int deg[RR];
+    [[maybe_unused]] uint32_t colw[RR][DC / 2], posw[RR][DC / 2];
+    [[maybe_unused]] P prev[2][RR][DC];
+    if constexpr (R > 0) {
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-        const int j = tid + r * kPPRole;
-        deg[r] = rs.cn_deg[j];
+        for (int r = 0; r < R; ++r) {
+            const int j = tid + r * kPPRole;
+            deg[r] = rs.cn_deg[j];
 #pragma unroll
-        for (int q = 0; q < DC / 8; ++q) {
-            const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)j * DC)[q];
-            const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)j * DC)[q];
-            colw[r][4 * q + 0] = xc.x; colw[r][4 * q + 1] = xc.y; colw[r][4 * q + 2] = xc.z; colw[r][4 * q + 3] = xc.w;
-            posw[r][4 * q + 0] = xp.x; posw[r][4 * q + 1] = xp.y; posw[r][4 * q + 2] = xp.z; posw[r][4 * q + 3] = xp.w;
-        }
-        if (deg[r] == 0)   // rows past M: gather the +0 entry, so their messages stay 0
-#pragma unroll
-            for (int q = 0; q < DC / 2; ++q) colw[r][q] = (uint32_t)(N + 2) * 0x10001u;
-    }
-    const double alpha = a.alpha, delta = a.delta, rcp = 1.0 / a.alpha;
-    const int npairs = (a.batch + 1) / 2;
-    [[maybe_unused]] P prev[2][RPT][DC];
-    PP_STAMP_DECL;
-    for (int grp = blockIdx.x; grp < npairs; grp += gridDim.x) {
-        int unc[2];
-        pp_channel<SRC>(a, s, N, grp, unc);
-        __syncthreads();   // B1: channel staged
-        if constexpr (!PREV_LDS) {
-#pragma unroll
-            for (int X = 0; X < 2; ++X)
-#pragma unroll
-                for (int r = 0; r < RPT; ++r)
-#pragma unroll
-                    for (int k = 0; k < DC; ++k) prev[X][r][k].v[0] = 0.0;
-        }
-        __syncthreads();   // B2: yq in app, padding slots zeroed (bit role)
-
-        // check nodes of slot X (row 1's reads issued before row 0 is computed)
-        auto check = [&](auto Xc) {
-            constexpr int X = decltype(Xc)::value;
-#pragma unroll
-            for (int r = 0; r < RPT; ++r)
-#pragma unroll
-                for (int q = 0; q < DC / 2; ++q) asm volatile("" : "+v"(colw[r][q]), "+v"(posw[r][q]));
-            const uint32_t ab = s.app_base[X], cb = s.c2v_base[X];
-            P xin[RPT][DC];
-            [[maybe_unused]] P pv[RPT][DC];
-            auto reads = [&](int r) {
-#pragma unroll
-                for (int k = 0; k < DC; ++k) xin[r][k] = lds_at<P>(addr8<DC>(colw[r], k, ab));
-                if constexpr (PREV_LDS) {
-#pragma unroll
-                    for (int k = 0; k < DC; ++k) pv[r][k] = lds_at<P>(addr8<DC>(posw[r], k, cb));
-                }
-            };
-#pragma unroll
-            for (int r = 0; r < (LDPC_PP_PREFETCH ? RPT : 1); ++r) reads(r);
-#pragma unroll
-            for (int r = 0; r < RPT; ++r) {
-                if (!LDPC_PP_PREFETCH && r > 0) reads(r);
-                P(&pr)[DC] = PREV_LDS ? pv[r] : prev[X][r];
-                bool ok = true;
-                if constexpr (LDPC_PP_EXP == 3) {
-#pragma unroll
-                    for (int k = 0; k < DC; ++k) pr[k].v[0] = xin[r][k].v[0] - pr[k].v[0];
-                } else {
-                    ok = cn_fast64<DC, VAR, FDIV>(xin[r], pr, alpha, rcp, delta);
-                }
-                if (!ok && deg[r] > 0) s.red[X] = 1;
-                if constexpr (LDPC_PP_EXP != 4) {
-#pragma unroll
-                    for (int k = 0; k < DC; ++k) lds_put<P>(addr8<DC>(posw[r], k, cb), pr[k]);
-                }
-                __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
+            for (int q = 0; q < DC / 8; ++q) {
+                const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)j * DC)[q];
+                const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)j * DC)[q];
+                colw[r][4 * q + 0] = xc.x; colw[r][4 * q + 1] = xc.y; colw[r][4 * q + 2] = xc.z; colw[r][4 * q + 3] = xc.w;
+                posw[r][4 * q + 0] = xp.x; posw[r][4 * q + 1] = xp.y; posw[r][4 * q + 2] = xp.z; posw[r][4 * q + 3] = xp.w;
             }
-        };
-        for (int it = 0; it < a.T; ++it) {
-            if (LDPC_PP_EXP != 2) check(std::integral_constant<int, 0>());
-            PP_BARRIER();   // | check(0,it) | bit(1,it-1) |
-            if (LDPC_PP_EXP != 2) check(std::integral_constant<int, 1>());
-            PP_BARRIER();   // | check(1,it) | bit(0,it) |
+            if (deg[r] == 0)   // rows past M: gather the +0 entry, so their messages stay 0
+#pragma unroll
+                for (int q = 0; q < DC / 2; ++q) colw[r][q] = (uint32_t)(N + 2) * 0x10001u;
         }
-        if (a.T > 0) PP_BARRIER();   // | -- | bit(1,T-1) |
-
-        // syndrome of both slots (padding edges read +inf: parity 0; rows past M skipped)
-        int sums[6] = {0, unc[0], 0, 0, unc[1], 0};
+    }
+    // bit slots of schedule thread bt
+    const int bt = tid - kPPRole;
+    [[maybe_unused]] int vgb[CPT], vgd[CPT];
+    [[maybe_unused]] uint32_t vdst2[(CPT + 1) / 2] = {};
+    if constexpr (HB) {
 #pragma unroll
-        for (int X = 0; X < 2; ++X) {
-            int synd = 0;
-#pragma unroll
-            for (int r = 0; r < RPT; ++r) {
-                int par = 0;
-#pragma unroll
-                for (int k = 0; k < DC; ++k) par ^= (s.app[X][u16_at<DC>(colw[r], k)].v[0] > 0.0) ? 0 : 1;
-                synd |= deg[r] > 0 ? par : 0;
-            }
-            sums[3 * X + 2] = synd;
+        for (int i = 0; i < CPT; ++i) {
+            const int c = rs.vn_col[bt * CPT + i];
+            vdst2[i / 2] |= (uint32_t)(c == 0xffff ? N + 1 : c) << (16 * (i & 1));
+            const uint32_t info = rs.vn_info[bt * CPT + i];
+            vgb[i] = __builtin_amdgcn_readfirstlane((int)(info & 0xffffu) - lane);
+            vgd[i] = __builtin_amdgcn_readfirstlane((int)(info >> 24));
         }
-        pp_account(a, s, grp, sums, redo, acc);
-    }
-    PP_STAMP_OUT()
-}
-
-// ---- the bit role: the bit slots of row-schedule thread t - 512, both slots ----
-template <int SRC, int CPT>
-__device__ __forceinline__ void pp_bit_role(const DecodeArgs &a, const DevGraph &g, const RowSched &rs,
-                                            const PPSlots &s, unsigned *redo, unsigned long long *acc, bool prev_lds)
-{
-    using P = Pack<double, 1>;
-    const int bt = threadIdx.x - kPPRole, N = g.N, lane = threadIdx.x & 63;
-    int vgb[CPT], vgd[CPT];
-    uint32_t vdst2[(CPT + 1) / 2] = {};
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-        const int c = rs.vn_col[bt * CPT + i];
-        vdst2[i / 2] |= (uint32_t)(c == 0xffff ? N + 1 : c) << (16 * (i & 1));
-        const uint32_t info = rs.vn_info[bt * CPT + i];
-        vgb[i] = __builtin_amdgcn_readfirstlane((int)(info & 0xffffu) - lane);
-        vgd[i] = __builtin_amdgcn_readfirstlane((int)(info >> 24));
-    }
-    auto vdst = [&](int i) -> int { return (int)((vdst2[i / 2] >> (16 * (i & 1))) & 0xffffu); };
-    const int EA = rs.e_pad + 64;
-    if (!prev_lds) {   // padding slots of the bit-node layout hold +0 (adding +0 changes no sum); never written
+        // padding slots of the bit-node layout hold +0 (adding +0 changes no sum); never written
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
             const int dg = (int)((rs.vn_info[bt * CPT + i] >> 16) & 0xffu);
@@ -334,79 +287,182 @@ __device__ __forceinline__ void pp_bit_role(const DecodeArgs &a, const DevGraph 
             for (int k = dg; k < gd; ++k) s.c2v[0][base + k * 64].v[0] = s.c2v[1][base + k * 64].v[0] = 0.0;
         }
     }
+    auto vdst = [&](int i) -> int { return (int)((vdst2[i / 2] >> (16 * (i & 1))) & 0xffffu); };
+    const double alpha = a.alpha, delta = a.delta, rcp = 1.0 / a.alpha;
     const int npairs = (a.batch + 1) / 2;
     PP_STAMP_DECL;
     for (int grp = blockIdx.x; grp < npairs; grp += gridDim.x) {
         int unc[2];
         pp_channel<SRC>(a, s, N, grp, unc);
-        if (prev_lds) {   // the check role re-reads its last messages: all c2v slots start at +0
-            for (int e = bt; e < EA; e += kPPRole) s.c2v[0][e].v[0] = s.c2v[1][e].v[0] = 0.0;
+        __syncthreads();   // B1: channel staged
+        [[maybe_unused]] P yq[2][CPT];
+        if constexpr (R > 0) {
+#pragma unroll
+            for (int X = 0; X < 2; ++X)
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) prev[X][r][k].v[0] = 0.0;
         }
-        __syncthreads();   // B1
-        P yq[2][CPT];
+        if constexpr (HB) {
 #pragma unroll
-        for (int X = 0; X < 2; ++X) {
-            bool in_ok = true;
+            for (int X = 0; X < 2; ++X) {
+                bool in_ok = true;
 #pragma unroll
-            for (int i = 0; i < CPT; ++i) {
-                // yq + 0 maps -0 to +0, so app is never -0 (fast64.h premise)
-                yq[X][i].v[0] = s.app[X][vdst(i) <= N ? vdst(i) : 0].v[0] + 0.0;
-                in_ok &= __builtin_fabs(yq[X][i].v[0]) < kFast64Max;
+                for (int i = 0; i < CPT; ++i) {
+                    // yq + 0 maps -0 to +0, so app is never -0 (fast64.h premise)
+                    yq[X][i].v[0] = s.app[X][vdst(i) <= N ? vdst(i) : 0].v[0] + 0.0;
+                    in_ok &= __builtin_fabs(yq[X][i].v[0]) < kFast64Max;
+                }
+#pragma unroll
+                for (int i = 0; i < CPT; ++i) s.app[X][vdst(i)] = yq[X][i];   // v2c = yq on the first pass (:364-370)
+                if (!in_ok) s.red[X] = 1;
             }
-#pragma unroll
-            for (int i = 0; i < CPT; ++i) s.app[X][vdst(i)] = yq[X][i];   // v2c = yq on the first pass (:364-370)
-            if (!in_ok) s.red[X] = 1;
+            if (tid == kPPRole) s.app[0][N].v[0] = s.app[1][N].v[0] = __builtin_huge_val();
+            if (tid == kPPRole + 1) s.app[0][N + 2].v[0] = s.app[1][N + 2].v[0] = 0.0;
         }
-        if (threadIdx.x == kPPRole) s.app[0][N].v[0] = s.app[1][N].v[0] = __builtin_huge_val();
-        if (threadIdx.x == kPPRole + 1) s.app[0][N + 2].v[0] = s.app[1][N + 2].v[0] = 0.0;
-        __syncthreads();   // B2
+        if (SYNC && tid == 0)
+#pragma unroll
+            for (int q = kPPCheckDone; q < kPPBitDone + 2; ++q) s.red[q] = 0;
+        __syncthreads();   // B2: yq in app
 
-        // bit nodes of slot Y: sum = yq + c2v in nlist order (:452-476)
-        auto bits = [&](auto Yc) {
-            constexpr int Y = decltype(Yc)::value;
+        // One barrier interval: the rows of slot X (their reads first), the bit
+        // nodes of slot 1 - X when `bits` (HB waves), then the rows' check nodes.
+        auto interval = [&](auto Xc, bool rows, bool bits) {
+            constexpr int X = decltype(Xc)::value, Y = 1 - X;
+            [[maybe_unused]] P xin[RR][DC];
+            if constexpr (R > 0) {
+                if (rows && LDPC_PP_EXP != 2) {
 #pragma unroll
-            for (int q = 0; q < (CPT + 1) / 2; ++q) asm volatile("" : "+v"(vdst2[q]));
-            P sum[CPT];
+                    for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int i = 0; i < CPT; ++i) sum[i] = yq[Y][i];
-            int k = 0;
-            const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-            vn_phases<double, 1, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum);
+                        for (int q = 0; q < DC / 2; ++q) asm volatile("" : "+v"(colw[r][q]), "+v"(posw[r][q]));
+                    const uint32_t ab = s.app_base[X];
 #pragma unroll
-            for (int i = 0; i < CPT; ++i) s.app[Y][vdst(i)] = sum[i];
+                    for (int r = 0; r < (LDPC_PP_PREFETCH ? R : 1); ++r)
+#pragma unroll
+                        for (int k = 0; k < DC; ++k)
+                            xin[r][k] = lds_at<P>((LDPC_PP_EXP == 5 || LDPC_PP_EXP == 7) ? ab + 8u * (uint32_t)(lane + 64 * (k + 8 * r))
+                                                                                         : addr8<DC>(colw[r], k, ab));
+                }
+            }
+            if constexpr (HB) {
+                if (LDPC_PP_BITDELAY > 0) __builtin_amdgcn_s_sleep(LDPC_PP_BITDELAY);
+                if (bits && LDPC_PP_EXP != 1) {   // bit nodes: sum = yq + c2v in nlist order (:452-476)
+#pragma unroll
+                    for (int q = 0; q < (CPT + 1) / 2; ++q) asm volatile("" : "+v"(vdst2[q]));
+                    P sum[CPT];
+#pragma unroll
+                    for (int i = 0; i < CPT; ++i) sum[i] = yq[Y][i];
+                    int k = 0;
+                    const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+                    vn_phases<double, 1, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum);
+#pragma unroll
+                    for (int i = 0; i < CPT; ++i) s.app[Y][vdst(i)] = sum[i];
+                }
+            }
+            if constexpr (R > 0) {
+                if (rows && LDPC_PP_EXP != 2) {
+                    const uint32_t ab = s.app_base[X], cb = s.c2v_base[X];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        if (!LDPC_PP_PREFETCH && r > 0) {
+#pragma unroll
+                            for (int k = 0; k < DC; ++k) xin[r][k] = lds_at<P>(addr8<DC>(colw[r], k, ab));
+                        }
+                        bool ok = true;
+                        if constexpr (LDPC_PP_EXP == 3) {
+#pragma unroll
+                            for (int k = 0; k < DC; ++k) prev[X][r][k].v[0] = xin[r][k].v[0] - prev[X][r][k].v[0];
+                        } else {
+                            ok = cn_fast64<DC, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta);
+                        }
+                        if (!ok && deg[r] > 0 && LDPC_PP_EXP == 0) s.red[X] = 1;   // experiments: never re-decode
+                        if constexpr (LDPC_PP_EXP != 4) {
+#pragma unroll
+                            for (int k = 0; k < DC; ++k)
+                                lds_put<P>((LDPC_PP_EXP == 6 || LDPC_PP_EXP == 7)
+                                               ? cb + 8u * (uint32_t)(lane + 64 * ((k + 8 * r + 16 * (tid >> 6)) % 112))
+                                               : addr8<DC>(posw[r], k, cb),
+                                           prev[X][r][k]);
+                        }
+                        if (R > 1) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
+                    }
+                }
+            }
         };
-        for (int it = 0; it < a.T; ++it) {
-            if (it > 0 && LDPC_PP_EXP != 1) bits(std::integral_constant<int, 1>());
-            PP_BARRIER();
-            if (LDPC_PP_EXP != 1) bits(std::integral_constant<int, 0>());
-            PP_BARRIER();
-        }
-        if (a.T > 0) {
-            if (LDPC_PP_EXP != 1) bits(std::integral_constant<int, 1>());
-            PP_BARRIER();
+        if constexpr (SYNC) {
+            // check(X, it) after bit(X, it-1) of all 8 bit waves; bit(X, it) after check(X, it)
+            static_assert(R == 0 || !HB, "dataflow sync: a wave holds rows or bit slots");
+            constexpr int W = kPPRole / 64;
+            for (int it = 0; it < a.T; ++it) {
+                if constexpr (R > 0) {
+                    pp_wait(s.red, kPPBitDone + 0, W * it);
+                    interval(std::integral_constant<int, 0>(), true, false);
+                    pp_signal(s.red, kPPCheckDone + 0);
+                    pp_wait(s.red, kPPBitDone + 1, W * it);
+                    interval(std::integral_constant<int, 1>(), true, false);
+                    pp_signal(s.red, kPPCheckDone + 1);
+                } else {
+                    pp_wait(s.red, kPPCheckDone + 0, W * (it + 1));
+                    interval(std::integral_constant<int, 1>(), false, true);   // bits of slot 0
+                    pp_signal(s.red, kPPBitDone + 0);
+                    pp_wait(s.red, kPPCheckDone + 1, W * (it + 1));
+                    interval(std::integral_constant<int, 0>(), false, true);   // bits of slot 1
+                    pp_signal(s.red, kPPBitDone + 1);
+                }
+            }
+            __syncthreads();
+        } else {
+            for (int it = 0; it < a.T; ++it) {
+                interval(std::integral_constant<int, 0>(), true, it > 0);
+                PP_BARRIER();   // | check(0,it) | bit(1,it-1) |
+                interval(std::integral_constant<int, 1>(), true, true);
+                PP_BARRIER();   // | check(1,it) | bit(0,it) |
+            }
+            if (a.T > 0) {
+                interval(std::integral_constant<int, 0>(), false, true);
+                PP_BARRIER();   // | -- | bit(1,T-1) |
+            }
         }
 
-        // decisions and error weight (:270, :382-393) of both slots
+        // syndrome (rows; padding edges read +inf: parity 0; rows past M skipped) and
+        // decisions / error weight (bit slots; :270, :382-393) of both slots
         int sums[6] = {0, unc[0], 0, 0, unc[1], 0};
 #pragma unroll
         for (int X = 0; X < 2; ++X) {
-            const int b = grp * 2 + X;
-            if (b >= a.batch) continue;
-            const int8_t *cvec = SRC == SRC_GIVEN ? (a.c ? a.c + (size_t)b * N : nullptr)
-                                                  : (a.cw_table ? a.cw_table + (size_t)((a.first_cw + (uint64_t)b) % (uint64_t)a.cw_rows) * N
-                                                                : nullptr);
-            int w = 0;
+            if constexpr (R > 0) {
+                int synd = 0;
 #pragma unroll
-            for (int i = 0; i < CPT; ++i) {
-                const int v = vdst(i);
-                if (v < N) {
-                    const int d = s.app[X][v].v[0] > 0.0 ? 1 : -1;   // :471-474
-                    const int cv = cvec ? cvec[v] : 1;
-                    w += (d != cv);
-                    if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+                for (int r = 0; r < R; ++r) {
+                    int par = 0;
+#pragma unroll
+                    for (int k = 0; k < DC; ++k) par ^= (s.app[X][u16_at<DC>(colw[r], k)].v[0] > 0.0) ? 0 : 1;
+                    synd |= deg[r] > 0 ? par : 0;
+                }
+                sums[3 * X + 2] = synd;
+            }
+            if constexpr (HB) {
+                const int b = grp * 2 + X;
+                if (b < a.batch) {
+                    const int8_t *cvec =
+                        SRC == SRC_GIVEN ? (a.c ? a.c + (size_t)b * N : nullptr)
+                                         : (a.cw_table ? a.cw_table + (size_t)((a.first_cw + (uint64_t)b) % (uint64_t)a.cw_rows) * N
+                                                       : nullptr);
+                    int w = 0;
+#pragma unroll
+                    for (int i = 0; i < CPT; ++i) {
+                        const int v = vdst(i);
+                        if (v < N) {
+                            const int d = s.app[X][v].v[0] > 0.0 ? 1 : -1;   // :471-474
+                            const int cv = cvec ? cvec[v] : 1;
+                            w += (d != cv);
+                            if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+                        }
+                    }
+                    sums[3 * X] = w;
                 }
             }
-            sums[3 * X] = w;
         }
         pp_account(a, s, grp, sums, redo, acc);
     }
@@ -415,25 +471,41 @@ __device__ __forceinline__ void pp_bit_role(const DecodeArgs &a, const DevGraph 
 
 }  // namespace
 
-template <int SRC, int DC, int CPT, int VAR, bool FDIV, bool PREV_LDS>
+#ifndef LDPC_PP_MODE
+#define LDPC_PP_MODE 0
+#endif
+// Experiments: s_nop instructions at the kernel entry shift the code that follows by 4 bytes
+// each (the code-layout sensitivity of the loops, with and without -falign-loops).
+#ifndef LDPC_PP_ENTRY_NOPS
+#define LDPC_PP_ENTRY_NOPS 0
+#endif
+
+template <int SRC, int DC, int CPT, int VAR, bool FDIV, int MODE>
 __global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph g, RowSched rs, unsigned *redo)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#pragma unroll
+    for (int i = 0; i < LDPC_PP_ENTRY_NOPS; ++i) asm volatile("s_nop 0");
     const PPSlots s = pp_slots(smem, g.N, rs.e_pad + 64);
     unsigned long long *acc = reinterpret_cast<unsigned long long *>(s.red + 128);   // thread 0's block totals
     if (threadIdx.x == 0) {
-        s.red[0] = s.red[1] = 0;
+        s.red[0] = s.red[1] = s.red[kPPSyncAbort] = 0;
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
     }
-    // the role is wave-uniform (an SGPR branch), so both sides meet every barrier
-    const bool checker = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < kPPRole / 64;
-    if (LDPC_PP_PRIO == 1 && checker) __builtin_amdgcn_s_setprio(1);
-    if (LDPC_PP_PRIO == 2 && !checker) __builtin_amdgcn_s_setprio(1);
-    if (checker)
-        pp_check_role<SRC, DC, VAR, FDIV, PREV_LDS>(a, g, rs, s, redo, acc);
-    else
-        pp_bit_role<SRC, CPT>(a, g, rs, s, redo, acc, PREV_LDS);
+    // the split is wave-uniform (an SGPR branch), so every wave meets every barrier
+    const bool low = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < kPPRole / 64;
+    if (LDPC_PP_PRIO == 1 && low) __builtin_amdgcn_s_setprio(1);
+    if (LDPC_PP_PRIO == 2 && !low) __builtin_amdgcn_s_setprio(1);
+    if (LDPC_PP_PRIO == 3 && ((threadIdx.x >> 8) & 1)) __builtin_amdgcn_s_setprio(1);
+    if constexpr (MODE == 1) {
+        if (low) pp_role<SRC, DC, CPT, VAR, FDIV, 1, false, false>(a, g, rs, s, redo, acc);
+        else pp_role<SRC, DC, CPT, VAR, FDIV, 1, true, false>(a, g, rs, s, redo, acc);
+    } else {   // 0: barrier intervals, 2: dataflow counters
+        if (low) pp_role<SRC, DC, CPT, VAR, FDIV, 2, false, MODE == 2>(a, g, rs, s, redo, acc);
+        else pp_role<SRC, DC, CPT, VAR, FDIV, 0, true, MODE == 2>(a, g, rs, s, redo, acc);
+    }
+    if (MODE == 2 && threadIdx.x == 0 && s.red[kPPSyncAbort]) atomicAdd(&a.counts[7], 1ull);   // host: error
     if (threadIdx.x == 0 && acc[3] > 0) {
         acc[4] = acc[3] * (unsigned long long)a.T;
 #pragma unroll
@@ -452,16 +524,13 @@ bool rows_pp_supported(const DevGraph &g, const RowSched &rs)
            rows_pp_lds_bytes(g, rs) <= 160 * 1024;
 }
 
-#ifndef LDPC_PP_PREV_LDS
-#define LDPC_PP_PREV_LDS 0
-#endif
-
 template <int SRC, int VAR, bool FDIV>
 static hipError_t launch_pp_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, unsigned *redo,
                               hipStream_t s, int num_cus)
 {
-    const bool prev_lds = std::getenv("LDPC_PP_PREV") ? std::getenv("LDPC_PP_PREV")[0] == 'l' : LDPC_PP_PREV_LDS;
-    auto fn = prev_lds ? k_rows_pp<SRC, 8, 4, VAR, FDIV, true> : k_rows_pp<SRC, 8, 4, VAR, FDIV, false>;
+    const int mode = std::getenv("LDPC_PP_MODE") ? std::atoi(std::getenv("LDPC_PP_MODE")) : LDPC_PP_MODE;
+    auto fn = mode == 1 ? k_rows_pp<SRC, 8, 4, VAR, FDIV, 1>
+              : mode == 2 ? k_rows_pp<SRC, 8, 4, VAR, FDIV, 2> : k_rows_pp<SRC, 8, 4, VAR, FDIV, 0>;
     const int lds = rows_pp_lds_bytes(g, rs);
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;

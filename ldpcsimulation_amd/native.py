@@ -87,7 +87,7 @@ class GdbfConfig:
     ymax: float = 2.5
     windowsize: int = 16
     nq: int = 16
-    precision: int = 0   # F32
+    precision: int = 1   # F64, the reference's double (decodeGDBF.cpp); F32 = 0 opt-in
     tswitch: int = 0     # MODESWITCH: Tswitch (:51)
     qsigma: float = 0.0  # QPROB, gdbf_decode only: the normalCDF sigma
 
@@ -101,7 +101,7 @@ class DecoderConfig:
     """Runtime form of the reference's compile-time decoder switches."""
     variant: int = MS            # MS | NMS (-D normalizedMS) | OMS (-D offsetMS)
     T: int = 10                  # iterations (fixed, no early termination)
-    precision: int = F32         # F32 throughput path | F64 reference-exact path
+    precision: int = F64         # F64 = the reference's double (default) | F32 throughput path (opt-in)
     alpha: float = 1.0           # NMS divisor
     delta: float = 0.0           # OMS offset
     quantize: bool = False       # -D quantizeSamples
@@ -163,6 +163,7 @@ def lib():
     vp, i32, i64, u32, u64, dbl = C.c_void_p, C.c_int, C.c_int64, C.c_uint32, C.c_uint64, C.c_double
     sig = {
         "ldpc_abi_version": ([], i32),
+        "ldpc_f64_nms_fast_division": ([dbl], i32),
         "ldpc_last_error": ([], C.c_char_p),
         "ldpc_graph_create": ([i32, i32, vp, vp, vp, vp, C.POINTER(vp)], i32),
         "ldpc_graph_load_alist": ([C.c_char_p, C.POINTER(vp)], i32),
@@ -220,7 +221,7 @@ def lib():
 
 
 # Every symbol include/ldpc_hip.h declares (checked by tests/test_abi.py).
-EXPORTED = ["ldpc_abi_version", "ldpc_last_error", "ldpc_graph_create", "ldpc_graph_load_alist",
+EXPORTED = ["ldpc_abi_version", "ldpc_f64_nms_fast_division", "ldpc_last_error", "ldpc_graph_create", "ldpc_graph_load_alist",
             "ldpc_graph_info", "ldpc_graph_destroy", "ldpc_graph_layers", "ldpc_device_count", "ldpc_ctx_create",
             "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
             "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",

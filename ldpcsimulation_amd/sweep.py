@@ -62,7 +62,9 @@ def parse(argv=None):
     p.add_argument("--no-early-stop", action="store_true", help="EMS: always run T iterations")
     p.add_argument("--max-frames", type=int, default=None)
     p.add_argument("--codewords", help="codeword file ('0'/'1' lines), as the reference's optional argument")
-    p.add_argument("--log", help="append the reference's tab-separated result line per point")
+    p.add_argument("--log", "--log-file", dest="log",
+                   help="append the reference's tab-separated result line per point (--log-file under torchrun, "
+                        "whose parser takes --log for a prefix of its own --log-dir)")
     p.add_argument("--json", action="store_true", help="also print one JSON object per point")
     p.add_argument("--sync", action="store_true",
                    help="one blocking round at a time (default: the next round decodes while one is reduced)")

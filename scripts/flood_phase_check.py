@@ -18,7 +18,8 @@ def main():
     g = native.Graph.from_alist(code_path("dvbs2_1_2.alist"))
     B = int(os.environ.get("BATCH", "2048"))
     ctx = native.Context(g, 0, B)
-    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=int(os.environ.get("T", "50")))
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=int(os.environ.get("T", "50")),
+                               precision=native.F64 if os.environ.get("PREC", "f32") == "f64" else native.F32)
     print("mode", os.environ.get("LDPC_FLOOD_MODE", "persistent"), ctx.kernel_info(cfg), flush=True)
     y, d, fr, cnt = ctx.sim_trace(1.0, 0.5, cfg, seed=3, stream_id=0, first_cw=0, batch=64)
     np.save(os.path.join(os.environ.get("OUT", "gpurun_out"), f"flood_d_{os.environ.get('LDPC_FLOOD_MODE', 'p')}.npy"), d)

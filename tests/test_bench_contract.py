@@ -84,6 +84,13 @@ def test_cpu_share_is_capped(monkeypatch):
     assert 1 <= b.cpu_share() <= 3
 
 
+def test_cpu_share_is_the_affinity_without_omp(monkeypatch):
+    """with OMP_NUM_THREADS unset the share is the whole affinity."""
+    b = _bench()
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    assert b.cpu_share() == len(os.sched_getaffinity(0)) == b.host_cores()
+
+
 def test_reference_fer_fixture():
     """tests/golden/reference_fer.json (scripts/ref_fer.py, the reference's own decodeNMS
     over 10 seeds per point): every seed ends by the stop rule (>= 40 frame errors,

@@ -49,3 +49,9 @@ def test_cli_precision_defaults_to_f64(tmp_path, cli, args, rng):
     p = subprocess.run([exe, code_path("80211n_1944_r12.alist")] + argv, env=env,
                        capture_output=True, text=True, timeout=60)
     assert "precision=f32" in p.stderr
+
+
+def test_python_configs_default_to_f64():
+    from ldpcsimulation_amd import native
+    assert native.DecoderConfig().precision == native.F64
+    assert native.GdbfConfig().precision == native.F64

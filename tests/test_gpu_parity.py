@@ -179,9 +179,14 @@ def test_all_kernels_bit_identical(monkeypatch, code):
         names = {k: c.kernel_info(cfg)["kernel"] for k, c in ctxs.items()}
         assert names["lds"] == "lds" and names["global"] == "global" and names["flood"] == "flood"
         if code != "4000.2000.4.244.alist":
-            # fp64: the fast-path row kernel (rows_fast.hip); fp32: the row kernel
-            assert names["default"] == ("rows_fast" if prec == native.F64 else "rows")
+            # fp64: the ping-pong kernel (rows_pp.hip, M in 513..1024) or the one-codeword
+            # fast-path kernel (rows_fast.hip); fp32: the row kernel
+            f64_default = "rows_pp" if code == "80211n_1944_r12.alist" else "rows_fast"
+            assert names["default"] == (f64_default if prec == native.F64 else "rows")
         outs = {k: c.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300) for k, c in ctxs.items()}
+        monkeypatch.setenv("LDPC_ROWS", "fast")   # fp64: the one-codeword fast kernel where pp is the default
+        outs["rows_fast"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
+        monkeypatch.delenv("LDPC_ROWS", raising=False)
         monkeypatch.setenv("LDPC_ROWS", "old")   # the previous row kernel (exact + fast loops in one)
         outs["rows_old"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
         monkeypatch.delenv("LDPC_ROWS", raising=False)

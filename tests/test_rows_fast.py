@@ -26,11 +26,23 @@ def test_markstein_division_matches_ieee(alpha):
     assert O.markstein_mismatch(alpha, 2_000_000, seed=11) == 0
 
 
-def test_markstein_alpha_gate():
-    """The kernel takes the fast division only for alpha it can prove (rows_fast.hip)."""
+@pytest.mark.parametrize("alpha,fast", [
+    (1.25, 1), (0.75, 1), (5.0, 1), (1.5, 1), (2.0 ** 60, 1), (3.0 * 2.0 ** 55, 1),
+    (1.1, 0), (2.0 ** -950, 0), (2.0 ** 61, 0), (3.0 * 2.0 ** 60, 0), (1.0 + 2.0 ** -30, 0),
+    (0.0, 0), (-1.25, 0), (float("inf"), 0), (float("nan"), 0)])
+def test_markstein_alpha_gate(alpha, fast):
+    """The kernel takes the fast division only for alpha it can prove (rows_fast.hip
+    markstein_exact_alpha, through ldpc_f64_nms_fast_division): alpha = P*2^E with odd
+    P < 2^20 and 2^-900 < alpha <= 2^60 (above 2^60 a minimum near 2^-960 divides to a
+    subnormal quotient); 1.1 and 1 + 2^-30 have P >= 2^20."""
     from ldpcsimulation_amd import native
-    ok = native.lib().ldpc_abi_version()  # library loads (no device needed)
-    assert ok == native.ABI_VERSION
+    assert native.lib().ldpc_f64_nms_fast_division(alpha) == fast
+
+
+@pytest.mark.parametrize("alpha", [2.0 ** 60, 3.0 * 2.0 ** 55])
+def test_markstein_division_matches_ieee_large_alpha(alpha):
+    """At the gate's upper end the fast division still equals IEEE x / alpha."""
+    assert O.markstein_mismatch(alpha, 500_000, seed=13) == 0
 
 
 class _FakeGraph:
@@ -68,10 +80,15 @@ def _glibc_frames(N, nframes, ebn0, R, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("code", ["80211n_1944_r12.alist", "PEGReg504x1008.alist"])
-def test_fast_kernel_is_the_f64_row_kernel(gpu_ctx_factory, code):
+def test_fast_kernel_is_the_f64_row_kernel(gpu_ctx_factory, monkeypatch, code):
+    """fp64 row graphs take a fast-path kernel: the ping-pong kernel (rows_pp.hip) for
+    the 802.11n code (M = 972: 512 threads x 2 rows), k_rows_fast otherwise or with
+    LDPC_ROWS=fast (the kernel the tests of this file exercise)."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(code)
     cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=5, precision=native.F64)
+    assert ctx.kernel_info(cfg)["kernel"] == ("rows_pp" if code == "80211n_1944_r12.alist" else "rows_fast")
+    monkeypatch.setenv("LDPC_ROWS", "fast")
     assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
     cfg.precision = native.F32                       # fp32: the row kernel by default
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
@@ -94,12 +111,14 @@ def test_f32_pair_fast_kernel_opt_in(gpu_ctx_factory, monkeypatch):
 @pytest.mark.parametrize("vname,v", [("ms", dict(variant=0)), ("nms", dict(variant=1, alpha=1.25)),
                                      ("nms_ieee", dict(variant=1, alpha=1.1)),
                                      ("oms", dict(variant=2, delta=0.15))])
-def test_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, code, vname, v):
+def test_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, code, vname, v):
     """Frames built to break the fast premise (|y| >= 2^1000, minima below 2^-960, inf,
     NaN, values growing past 2^1000 mid-decode) are re-decoded on the exact path:
     decisions, error weights and counters equal the fp64 oracle's for every frame,
-    and the re-decode list holds exactly the frames that broke it."""
+    and the re-decode list holds exactly the frames that broke it. (k_rows_fast; the
+    ping-pong kernel's twin is tests/test_rows_pp.py.)"""
     from ldpcsimulation_amd import native
+    monkeypatch.setenv("LDPC_ROWS", "fast")
     ctx = gpu_ctx_factory(code)
     N = ctx.graph.N
     y = _glibc_frames(N, 16, 1.5, 0.5, seed=4242)
@@ -170,13 +189,17 @@ def test_f32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, 
 @pytest.mark.gpu
 @pytest.mark.parametrize("ebn0", [1.5, 1.75])
 @pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0))])
-def test_f64_headline_config_bit_exact(gpu_ctx_factory, ebn0, vname, v):
+@pytest.mark.parametrize("kernel", ["pp", "fast"])
+def test_f64_headline_config_bit_exact(gpu_ctx_factory, monkeypatch, kernel, ebn0, vname, v):
     """The bench configuration in fp64 (802.11n N=1944, T=50, on-device Philox channel):
     2048 codewords per point, decisions identical to the fp64 oracle on the same y,
-    and no codeword needed the exact path."""
+    and no codeword needed the exact path -- for the bench's kernel (the ping-pong
+    kernel, rows_pp.hip) and for k_rows_fast."""
     from ldpcsimulation_amd import native
+    monkeypatch.setenv("LDPC_ROWS", kernel)
     ctx = gpu_ctx_factory("80211n_1944_r12.alist")
     cfg = native.DecoderConfig(T=50, precision=native.F64, **v)
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_" + kernel
     y, d, fr, cnt = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261016, stream_id=1, first_cw=0, batch=2048)
     assert ctx.redo_count() == 0
     want = O.Alist(code_path("80211n_1944_r12.alist")).decode(y, 50, O.Cfg(**v), workers=16)

@@ -34,6 +34,7 @@ def test_pp_kernel_selected_for_the_bench_code(gpu_ctx_factory, monkeypatch):
     _kernel(monkeypatch, "fast")
     assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
     monkeypatch.delenv("LDPC_ROWS")
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"      # the default
     # PEG 504x1008 has M <= 512: one row per thread, the one-codeword kernel
     assert gpu_ctx_factory("PEGReg504x1008.alist").kernel_info(cfg)["kernel"] == "rows_fast"
 

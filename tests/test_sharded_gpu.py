@@ -14,8 +14,11 @@ frame-by-frame run of the same noise.
 Config 3's sweep (sweep.py --schedule layered: DVB-S2 N=64800, layered NMS,
 the global layered kernel) is run the same way, two ranks against one, at one
 SNR point of the sweep."""
+import json
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -24,14 +27,14 @@ from conftest import code_path
 
 CODE = "80211n_1944_r12.alist"
 EBN0, SEED, T = 1.5, 20261018, 50
-# config 3: DVB-S2 layered, one point of the SNR sweep (fp32, the sweep's default precision)
+# config 3: DVB-S2 layered, one point of the SNR sweep (fp64, the sweep's default precision)
 DVB_CODE, DVB_EBN0, DVB_T = "dvbs2_1_2.alist", 1.0, 10
 
 
 def _cfg(case="c2"):
     from ldpcsimulation_amd import native
     if case == "c3":
-        return native.DecoderConfig(variant=native.NMS, alpha=1.25, T=DVB_T, precision=native.F32,
+        return native.DecoderConfig(variant=native.NMS, alpha=1.25, T=DVB_T, precision=native.F64,
                                     schedule=native.LAYERED)
     return native.DecoderConfig(variant=native.NMS, alpha=1.25, T=T, precision=native.F64)
 
@@ -132,3 +135,45 @@ def test_dvbs2_layered_sweep_point_two_ranks_equal_one_rank(gpu_ctx_factory):
         assert isinstance(counts, dict), counts
         assert counts == one.counts, (rank, counts, one.counts)
         assert np.array_equal(np.array(hist), one.hist), rank
+
+
+@pytest.mark.gpu
+def test_sweep_main_two_ranks(tmp_path):
+    """sweep.main itself with two ranks (torch.distributed.run as a
+    child process, gloo, both ranks on the box's one GPU) and no --seed: the ranks key
+    their noise with rank 0's seed (broadcast), rank 0 alone appends one reference-format
+    log line per point (decodeMinSum.cpp:313-329), and the counts equal a one-rank run
+    with that seed."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    log2 = tmp_path / "two.txt"
+    args = [code_path(CODE), "--rate", "0.5", "--snr", "1.25", "1.5", "-T", "50", "--variant", "nms",
+            "--alpha", "1.25", "--batch", "2048", "--json"]
+    env = dict(os.environ, LDPC_SWEEP_REPORT_SEED="1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        "-m", "ldpcsimulation_amd.sweep"] + args + ["--backend", "gloo", "--share-device",
+                                                                    "--log-file", str(log2)],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    seeds = {}
+    for line in p.stderr.splitlines():
+        i = line.find('{"rank"')
+        if i >= 0:
+            d = json.loads(line[i:])
+            seeds[d["rank"]] = d["seed"]
+    assert set(seeds) == {0, 1} and seeds[0] == seeds[1], seeds
+    lines = log2.read_text().splitlines()
+    assert len(lines) == 2, lines                       # rank 0 only, one line per point
+    assert [l.split("\t")[0] for l in lines] == ["1.25", "1.5"]
+    two = [json.loads(l[l.index("{"):]) for l in p.stdout.splitlines() if '"ebn0_db"' in l]
+    assert len(two) == 2 and all(d["n_gpus"] == 2 and d["precision"] == "f64" for d in two)
+    log1 = tmp_path / "one.txt"
+    q = subprocess.run([sys.executable, "-m", "ldpcsimulation_amd.sweep"] + args +
+                       ["--seed", str(seeds[0]), "--log", str(log1)], cwd=root, capture_output=True, text=True,
+                       timeout=600)
+    assert q.returncode == 0, q.stderr[-3000:]
+    one = [json.loads(l[l.index("{"):]) for l in q.stdout.splitlines() if '"ebn0_db"' in l]
+    keys = ("bit_err", "frame_err", "uncoded_bit_err", "frames", "iters", "syndrome_fail")
+    for a, b in zip(two, one):
+        assert {k: a[k] for k in keys} == {k: b[k] for k in keys}, (a, b)
+    assert log1.read_text().splitlines() == lines
