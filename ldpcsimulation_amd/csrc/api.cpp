@@ -366,6 +366,7 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
             c->fs.dc = fh.dc;
             c->fs.ngroups = fh.ngroups;
             c->fs.e_pad = fh.e_pad;
+            c->fs.dv = g->maxdv;
             c->fs.sp = (const int32_t *)fb;
             c->fs.sq = (const int32_t *)(fb + o_sq);
             c->fs.rdeg = (const uint8_t *)(fb + o_rd);

@@ -53,6 +53,7 @@ struct RowSched {
 // Device copy of graph.h's FloodSchedule (global-memory flooding kernel).
 struct FloodSched {
     int M_pad, dc, ngroups, e_pad;
+    int dv;                         // max column degree
     const int32_t *sp, *sq;         // [dc * M_pad] slot-major bit position / c2v element
     const uint8_t *rdeg;            // [M_pad]
     const int32_t *pos_of_bit;      // [N]

@@ -656,7 +656,11 @@ __global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs
     }
 }
 
-template <typename F>
+// DV = a bound on the column degree: the d loads of a bit are issued together
+// (one memory round trip per slot instead of d dependent ones; the adds stay in
+// nlist order), and two slots are in flight per step. DV = 0: any degree, one
+// load at a time.
+template <typename F, int DV>
 __global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char *scratch, size_t slot_bytes, int nres)
 {
     const int NP = fs.ngroups * 64;
@@ -669,12 +673,36 @@ __global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char 
     const int d = fs.pdeg[p];
     if (d == 0) return;
     const int off = fs.gbase[p >> 6] + (p & 63);
-    for (int r = r0; r < nres; r += rs) {
-        const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
-        const F *cp = S.c2v + off;
-        F sum = S.yq[p];
-        for (int e = 0; e < d; ++e) sum += cp[64 * e];   // nlist order (:452-476)
-        S.app[p] = sum;
+    if constexpr (DV == 0) {
+        for (int r = r0; r < nres; r += rs) {
+            const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
+            const F *cp = S.c2v + off;
+            F sum = S.yq[p];
+            for (int e = 0; e < d; ++e) sum += cp[64 * e];   // nlist order (:452-476)
+            S.app[p] = sum;
+        }
+    } else {
+        for (int r = r0; r < nres; r += 2 * rs) {
+            const bool two = r + rs < nres;
+            const auto S0 = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
+            const auto S1 = FloodSlot::at<F>(scratch, slot_bytes, two ? r + rs : r, fs);
+            F v0[DV], v1[DV];
+            const F y0 = S0.yq[p], y1 = S1.yq[p];
+#pragma unroll
+            for (int e = 0; e < DV; ++e) {
+                v0[e] = e < d ? S0.c2v[off + 64 * e] : F(0);
+                v1[e] = e < d ? S1.c2v[off + 64 * e] : F(0);
+            }
+            F s0 = y0, s1 = y1;
+#pragma unroll
+            for (int e = 0; e < DV; ++e)
+                if (e < d) {   // nlist order (:452-476)
+                    s0 += v0[e];
+                    s1 += v1[e];
+                }
+            S0.app[p] = s0;
+            if (two) S1.app[p] = s1;
+        }
     }
 }
 
@@ -800,7 +828,13 @@ struct FloodHalf {
 #else
         const dim3 bg((NP + 255) / 256, (n + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW);
 #endif
-        hipLaunchKernelGGL((k_flood_bit<F>), bg, dim3(256), 0, s, *fs, scratch + sb * (size_t)lo, sb, n);
+        unsigned char *sc = scratch + sb * (size_t)lo;
+        if (fs->dv <= 8)
+            hipLaunchKernelGGL((k_flood_bit<F, 8>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+        else if (fs->dv <= 16)
+            hipLaunchKernelGGL((k_flood_bit<F, 16>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+        else
+            hipLaunchKernelGGL((k_flood_bit<F, 0>), bg, dim3(256), 0, s, *fs, sc, sb, n);
     }
     void end(int b0) const
     {
@@ -814,7 +848,12 @@ struct FloodHalf {
     }
 };
 
-// LDPC_FLOOD_STREAMS=2: the resident set in two halves on two streams (aux).
+// The resident set in two halves on two streams (aux): one half's launch
+// boundaries and its small init / finish / accounting launches overlap the other
+// half's phase kernels. The single stream is 95 % busy already
+// (profiles/r03_dvbs2_flood_gaps.json).
+// LDPC_FLOOD_STREAMS=2 (opt-in): measured +6 % while the bit kernel's loads were
+// serialised, 7 % slower once they are batched (1 855 vs 2 000 Mbit/s).
 static bool flood_two_streams()
 {
     const char *e = std::getenv("LDPC_FLOOD_STREAMS");
@@ -1193,9 +1232,9 @@ __global__ __launch_bounds__(512) void k_decode_layered_lds(DecodeArgs a, DevGra
 // positions [0, P) (dynamic LDS, (P + 1) * sizeof(F) bytes) -- DVB-S2 keeps
 // 19 455 of its 64 800 bits there, every degree-8 bit and a third of the
 // degree-3 ones, 54 % of the edge gathers and scatters.
-template <typename F, int SRC, int DC, int R, bool SPLIT>
-__global__ __launch_bounds__(512) void k_decode_layered_global(DecodeArgs a, DevGraph g, FloodSched fs, LayerSched ls,
-                                                               unsigned char *scratch, size_t slot_bytes, int P)
+template <typename F, int SRC, int DC, int R, bool SPLIT, int NT = 512>
+__global__ __launch_bounds__(NT) void k_decode_layered_global(DecodeArgs a, DevGraph g, FloodSched fs, LayerSched ls,
+                                                              unsigned char *scratch, size_t slot_bytes, int P)
 {
     using F2 = typename F2T<F>::T;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1872,7 +1911,23 @@ static int layered_r64()
     const char *e = std::getenv("LDPC_LAYERED_R64");
     return (e && std::atoi(e) == 1) ? 1 : 2;
 }
-static int layered_rows_per_pass(bool global, bool f64) { return global ? (f64 ? layered_r64() : 4) : 1; }
+// Threads of the global layered kernel: 1024 (4 waves per SIMD at <= 128 VGPRs,
+// R = 2 rows per thread per pass in fp32, 1 in fp64) -- DVB-S2 T=50: fp32 59.4 ->
+// 42.7 ms, fp64 87.4 -> 74.2 ms per 2,048 codewords against 512 threads (2 waves
+// per SIMD at ~256 VGPRs, R = 4 / 2: the same rows in flight per pass, half the
+// waves to hide the L2 / Infinity Cache latency); LDPC_LAYERED_THREADS=512 keeps
+// the latter.
+static int layered_nt()
+{
+    const char *e = std::getenv("LDPC_LAYERED_THREADS");
+    return (e && std::atoi(e) == 512) ? 512 : 1024;
+}
+static int layered_rows_per_pass(bool global, bool f64)
+{
+    if (!global) return 1;
+    if (layered_nt() == 1024) return f64 ? 1 : 2;
+    return f64 ? layered_r64() : 4;
+}
 
 static int layered_threads(const LayerSched &ls, int R, int cap)
 {
@@ -1896,7 +1951,7 @@ KernelChoice choose_layered(const DevGraph &g, bool f64, const FloodSched &fs, c
     } else {
         kc.name = "layered_global";
         kc.scratch_per_block = st;
-        kc.threads = layered_threads(ls, layered_rows_per_pass(true, f64), 512);
+        kc.threads = layered_threads(ls, layered_rows_per_pass(true, f64), layered_nt());
     }
     return kc;
 }
@@ -1923,8 +1978,14 @@ static hipError_t launch_layered_t(const DecodeArgs &a, const DevGraph &g, const
         constexpr bool SPLIT = sizeof(F) == 8;
         const int r = layered_rows_per_pass(true, sizeof(F) == 8);
         decltype(&k_decode_layered_global<F, SRC, DC, 1, SPLIT>) fn;
-        if constexpr (sizeof(F) == 4) fn = k_decode_layered_global<F, SRC, DC, 4, SPLIT>;
-        else fn = r == 2 ? k_decode_layered_global<F, SRC, DC, 2, SPLIT> : k_decode_layered_global<F, SRC, DC, 1, SPLIT>;
+        if (kc.threads > 512) {   // LDPC_LAYERED_THREADS=1024
+            if constexpr (sizeof(F) == 4) fn = k_decode_layered_global<F, SRC, DC, 2, SPLIT, 1024>;
+            else fn = k_decode_layered_global<F, SRC, DC, 1, SPLIT, 1024>;
+        } else if constexpr (sizeof(F) == 4) {
+            fn = k_decode_layered_global<F, SRC, DC, 4, SPLIT>;
+        } else {
+            fn = r == 2 ? k_decode_layered_global<F, SRC, DC, 2, SPLIT> : k_decode_layered_global<F, SRC, DC, 1, SPLIT>;
+        }
         const int P = SPLIT ? layered_lds_positions(fs.ngroups * 64 + 1, sizeof(F)) : 0;
         const int lds = SPLIT ? (P + 1) * (int)sizeof(F) : 0;   // + LayApp's dummy slot
         hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -1961,8 +2022,11 @@ hipError_t launch_layered(const DevGraph &g, const DecodeArgs &a, bool f64, cons
 int layered_blocks_per_cu(bool f64, const KernelChoice &kc)
 {
     int nb = 0;
-    const void *fn = f64 ? (const void *)k_decode_layered_global<double, SRC_PHILOX, 8, 2, true>
-                         : (const void *)k_decode_layered_global<float, SRC_PHILOX, 8, 4, false>;
+    const void *fn = kc.threads > 512
+                         ? (f64 ? (const void *)k_decode_layered_global<double, SRC_PHILOX, 8, 1, true, 1024>
+                                : (const void *)k_decode_layered_global<float, SRC_PHILOX, 8, 2, false, 1024>)
+                         : (f64 ? (const void *)k_decode_layered_global<double, SRC_PHILOX, 8, 2, true>
+                                : (const void *)k_decode_layered_global<float, SRC_PHILOX, 8, 4, false>);
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, kc.threads,
         f64 ? (layered_lds_positions(1 << 30, 8) + 1) * 8 : 0);
     if (e != hipSuccess) { (void)hipGetLastError(); return 0; }

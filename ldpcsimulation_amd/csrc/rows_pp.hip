@@ -58,6 +58,10 @@ namespace {
 #ifndef LDPC_PP_BITDELAY
 #define LDPC_PP_BITDELAY 0
 #endif
+// 0: no scheduling fence between a check wave's two rows (the compiler may interleave them)
+#ifndef LDPC_PP_ROWFENCE
+#define LDPC_PP_ROWFENCE 1
+#endif
 
 // Wave priority (s_setprio): 0 none, 1 check role above the bit role, 2 the reverse,
 // 3 the younger half of each role (waves 4-7, 12-15) above the older half.
@@ -386,7 +390,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                                                : addr8<DC>(posw[r], k, cb),
                                            prev[X][r][k]);
                         }
-                        if (R > 1) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
+                        if (R > 1 && LDPC_PP_ROWFENCE) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
                     }
                 }
             }
