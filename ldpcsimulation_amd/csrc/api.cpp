@@ -352,7 +352,13 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
                          n_ba = fh.bit_at.size(), n_pd = fh.pdeg.size(), n_gb = fh.gbase.size();
             const size_t o_sq = al(4 * n_sp), o_rd = o_sq + al(4 * n_sp), o_pb = o_rd + al(n_rd),
                          o_ba = o_pb + al(4 * n_pb), o_pd = o_ba + al(4 * n_ba), o_gb = o_pd + al(n_pd),
-                         tot = o_gb + al(4 * n_gb);
+                         o_er = o_gb + al(4 * n_gb), n_er = (size_t)fh.e_pad + 64, tot = o_er + al(4 * n_er);
+            // element -> (row, position) of the c2v layout: the packed-message bit phase
+            // (kernels.hip k_flood_bit_packed) rebuilds a message from its row's state
+            std::vector<uint32_t> eref(n_er, 0);
+            for (int i = 0; i < fh.M_pad; ++i)
+                for (int k = 0; k < fh.rdeg[i]; ++k)
+                    eref[fh.sq[(size_t)k * fh.M_pad + i]] = ((uint32_t)i << 5) | (uint32_t)k;
             CTX_TRY(c->fsched.ensure(tot));
             unsigned char *fb = (unsigned char *)c->fsched.p;
             CTX_TRY(hipMemcpy(fb, fh.sp.data(), 4 * n_sp, hipMemcpyHostToDevice));
@@ -362,6 +368,7 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
             CTX_TRY(hipMemcpy(fb + o_ba, fh.bit_at.data(), 4 * n_ba, hipMemcpyHostToDevice));
             CTX_TRY(hipMemcpy(fb + o_pd, fh.pdeg.data(), n_pd, hipMemcpyHostToDevice));
             CTX_TRY(hipMemcpy(fb + o_gb, fh.gbase.data(), 4 * n_gb, hipMemcpyHostToDevice));
+            CTX_TRY(hipMemcpy(fb + o_er, eref.data(), 4 * n_er, hipMemcpyHostToDevice));
             c->fs.M_pad = fh.M_pad;
             c->fs.dc = fh.dc;
             c->fs.ngroups = fh.ngroups;
@@ -374,6 +381,7 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
             c->fs.bit_at = (const int32_t *)(fb + o_ba);
             c->fs.pdeg = (const uint8_t *)(fb + o_pd);
             c->fs.gbase = (const int32_t *)(fb + o_gb);
+            c->fs.eref = (const uint32_t *)(fb + o_er);
             c->has_fs = true;
             ldpc::LayerSchedule lh;
             if (fh.dc <= ldpc::kPackedMaxDc && ldpc::build_layers(*g, fh, lh).empty()) {
@@ -928,6 +936,10 @@ int ldpc_ctx_row_sched_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, int32_t *i
     info[5] = kc.cw_per_block;
     info[6] = kc.lds_bytes;
     info[7] = ldpc::blocks_per_cu(c->dg, f64, kc);
+    if (f64 && use_rows_fast(c, kc, f64, ldpc::DecodeArgs{}) && use_rows_pp(c, f64)) {   // one 1024-thread block per CU
+        info[6] = ldpc::rows_pp_lds_bytes(c->dg, c->rs);
+        info[7] = 1;
+    }
     return LDPC_OK;
 }
 
@@ -964,6 +976,10 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
     if (bpc) *bpc = cfg->variant == LDPC_BP ? 0 : is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
                                    : ldpc::blocks_per_cu(c->dg, f64, kc);
+    if (cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64, a) && use_rows_pp(c, f64)) {
+        if (lds_bytes) *lds_bytes = ldpc::rows_pp_lds_bytes(c->dg, c->rs);
+        if (bpc) *bpc = 1;
+    }
     return LDPC_OK;
 }
 

@@ -60,6 +60,7 @@ struct FloodSched {
     const int32_t *bit_at;          // [ngroups * 64]
     const uint8_t *pdeg;            // [ngroups * 64]
     const int32_t *gbase;           // [ngroups]
+    const uint32_t *eref;           // [e_pad + 64] per c2v element: (row << 5) | position in the row
 };
 
 // Device copy of graph.h's LayerSchedule.

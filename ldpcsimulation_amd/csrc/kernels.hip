@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace ldpc {
@@ -578,38 +579,15 @@ __global__ __launch_bounds__(256) void k_flood_init(DecodeArgs a, DevGraph g, Fl
 // Codewords per thread of the phase kernels: the row's (or bit position's)
 // schedule is loaded once and used for CPW resident codewords (slots
 // blockIdx.y + j * gridDim.y).
-template <typename F, int DC>
-__global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs, unsigned char *scratch,
-                                                     size_t slot_bytes, int nres)
+//
+// The check node of k_decode_flood (:410-450, :494-515) on one resident slot:
+// xa = the gathered app values, (old, om) = the row's packed state.
+template <typename F, int DC, bool C2V>
+__device__ __forceinline__ void flood_cn(const DecodeArgs &a, const FloodSlot::View<F> &S, int i, int deg,
+                                         const int (&sq)[DC], const F (&xa)[DC], typename F2T<F>::T old, uint32_t om)
 {
     using F2 = typename F2T<F>::T;
-    const int MP = fs.M_pad, NP = fs.ngroups * 64;
-#if LDPC_FLOOD_XCD
-    // XCD-aware: blocks b and b + 8 share an XCD (round-robin placement, speed
-    // only); XCD x decodes the slots x, x + 8, ... one after the other, all
-    // rows of a slot at once, so the ~3.5 gathers of each app value hit its L2.
-    const int i = (blockIdx.x >> 3) * blockDim.x + threadIdx.x, r0 = blockIdx.x & 7, rs = 8;
-#else
-    const int i = blockIdx.x * blockDim.x + threadIdx.x, r0 = blockIdx.y, rs = gridDim.y;
-#endif
-    if (i >= MP) return;
-    const int deg = fs.rdeg[i];
-    if (deg == 0) return;
     const F alpha = (F)a.alpha, delta = (F)a.delta;
-    int sp[DC], sq[DC];
-#pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        sp[k] = k < deg ? fs.sp[(size_t)k * MP + i] : NP;
-        sq[k] = k < deg ? fs.sq[(size_t)k * MP + i] : 0;
-    }
-    for (int r = r0; r < nres; r += rs) {
-    const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
-    F xa[DC];
-#pragma unroll
-    for (int k = 0; k < DC; ++k) xa[k] = S.app[sp[k]];
-    const F2 old = S.m12[i];
-    const uint32_t om = S.meta[i];
-    // ---- the check node of k_decode_flood (:410-450, :494-515) ----
     const int oidx = (int)(om & 31u);
     F mn1 = dinf<F>(), mn2 = dinf<F>();
     int amin = 31;
@@ -646,21 +624,78 @@ __global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs
     nw.y = M2;
     S.m12[i] = nw;
     S.meta[i] = (uint32_t)amin | (eff << 5);
+    if constexpr (C2V) {
 #pragma unroll
-    for (int k = 0; k < DC; ++k) {
-        if (k < deg) {
-            const F mag = (k == amin) ? M2 : M1;
-            S.c2v[sq[k]] = ((eff >> k) & 1u) ? -mag : mag;
+        for (int k = 0; k < DC; ++k) {
+            if (k < deg) {
+                const F mag = (k == amin) ? M2 : M1;
+                S.c2v[sq[k]] = ((eff >> k) & 1u) ? -mag : mag;
+            }
         }
     }
+}
+
+// The c2v message of position k of a row with packed state (m, meta): exactly
+// the value flood_cn stores (magnitude M2 at the argmin, M1 elsewhere, signed
+// by the row's sign bit k).
+template <typename F>
+__device__ __forceinline__ F flood_msg(typename F2T<F>::T m, uint32_t meta, uint32_t k)
+{
+    const F mag = (k == (meta & 31u)) ? m.y : m.x;
+    return ((meta >> (5 + k)) & 1u) ? -mag : mag;
+}
+
+// SPS resident slots per step: their gathers are issued together (one memory
+// round trip for SPS slots), the check nodes then run slot by slot.
+template <typename F, int DC, int SPS, bool C2V>
+__global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs, unsigned char *scratch,
+                                                     size_t slot_bytes, int nres)
+{
+    using F2 = typename F2T<F>::T;
+    const int MP = fs.M_pad, NP = fs.ngroups * 64;
+#if LDPC_FLOOD_XCD
+    // XCD-aware: blocks b and b + 8 share an XCD (round-robin placement, speed
+    // only); XCD x decodes the slots x, x + 8, ... one after the other, all
+    // rows of a slot at once, so the ~3.5 gathers of each app value hit its L2.
+    const int i = (blockIdx.x >> 3) * blockDim.x + threadIdx.x, r0 = blockIdx.x & 7, rs = 8;
+#else
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, r0 = blockIdx.y, rs = gridDim.y;
+#endif
+    if (i >= MP) return;
+    const int deg = fs.rdeg[i];
+    if (deg == 0) return;
+    int sp[DC], sq[DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+        sp[k] = k < deg ? fs.sp[(size_t)k * MP + i] : NP;
+        sq[k] = k < deg ? fs.sq[(size_t)k * MP + i] : 0;
+    }
+    for (int r = r0; r < nres; r += SPS * rs) {
+        F xa[SPS][DC];
+        F2 old[SPS];
+        uint32_t om[SPS];
+#pragma unroll
+        for (int j = 0; j < SPS; ++j) {
+            const int rr = r + j * rs < nres ? r + j * rs : r;   // past the end: a harmless re-read of slot r
+            const auto S = FloodSlot::at<F>(scratch, slot_bytes, rr, fs);
+#pragma unroll
+            for (int k = 0; k < DC; ++k) xa[j][k] = S.app[sp[k]];
+            old[j] = S.m12[i];
+            om[j] = S.meta[i];
+        }
+#pragma unroll
+        for (int j = 0; j < SPS; ++j)
+            if (r + j * rs < nres)
+                flood_cn<F, DC, C2V>(a, FloodSlot::at<F>(scratch, slot_bytes, r + j * rs, fs), i, deg, sq, xa[j],
+                                     old[j], om[j]);
     }
 }
 
 // DV = a bound on the column degree: the d loads of a bit are issued together
 // (one memory round trip per slot instead of d dependent ones; the adds stay in
-// nlist order), and two slots are in flight per step. DV = 0: any degree, one
+// nlist order), and SPS slots are in flight per step. DV = 0: any degree, one
 // load at a time.
-template <typename F, int DV>
+template <typename F, int DV, int SPS>
 __global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char *scratch, size_t slot_bytes, int nres)
 {
     const int NP = fs.ngroups * 64;
@@ -682,26 +717,73 @@ __global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char 
             S.app[p] = sum;
         }
     } else {
-        for (int r = r0; r < nres; r += 2 * rs) {
-            const bool two = r + rs < nres;
-            const auto S0 = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
-            const auto S1 = FloodSlot::at<F>(scratch, slot_bytes, two ? r + rs : r, fs);
-            F v0[DV], v1[DV];
-            const F y0 = S0.yq[p], y1 = S1.yq[p];
+        for (int r = r0; r < nres; r += SPS * rs) {
+            F v[SPS][DV], y[SPS];
 #pragma unroll
-            for (int e = 0; e < DV; ++e) {
-                v0[e] = e < d ? S0.c2v[off + 64 * e] : F(0);
-                v1[e] = e < d ? S1.c2v[off + 64 * e] : F(0);
+            for (int j = 0; j < SPS; ++j) {
+                const auto S = FloodSlot::at<F>(scratch, slot_bytes, r + j * rs < nres ? r + j * rs : r, fs);
+                y[j] = S.yq[p];
+#pragma unroll
+                for (int e = 0; e < DV; ++e) v[j][e] = e < d ? S.c2v[off + 64 * e] : F(0);
             }
-            F s0 = y0, s1 = y1;
+#pragma unroll
+            for (int j = 0; j < SPS; ++j) {
+                F sum = y[j];
+#pragma unroll
+                for (int e = 0; e < DV; ++e)
+                    if (e < d) sum += v[j][e];   // nlist order (:452-476)
+                if (r + j * rs < nres) FloodSlot::at<F>(scratch, slot_bytes, r + j * rs, fs).app[p] = sum;
+            }
+        }
+    }
+}
+
+// Bit phase without the c2v array (LDPC_FLOOD_MSG=packed, the default): each
+// message is rebuilt from its row's packed state (m12, meta), gathered through
+// the element -> (row, position) table eref. The check phase then writes only
+// the 12 (fp32) / 20 (fp64) bytes of state per row instead of dc messages, and
+// the bit phase reads each row's state once per L2 instead of a message per
+// edge -- the same sums, in nlist order, of the same values.
+template <typename F, int DV, int SPS>
+__global__ __launch_bounds__(256) void k_flood_bit_packed(FloodSched fs, unsigned char *scratch, size_t slot_bytes,
+                                                          int nres)
+{
+    using F2 = typename F2T<F>::T;
+    const int NP = fs.ngroups * 64;
+#if LDPC_FLOOD_XCD
+    const int p = (blockIdx.x >> 3) * blockDim.x + threadIdx.x, r0 = blockIdx.x & 7, rs = 8;
+#else
+    const int p = blockIdx.x * blockDim.x + threadIdx.x, r0 = blockIdx.y, rs = gridDim.y;
+#endif
+    if (p >= NP) return;
+    const int d = fs.pdeg[p];
+    if (d == 0) return;
+    const int off = fs.gbase[p >> 6] + (p & 63);
+    uint32_t ref[DV];
+#pragma unroll
+    for (int e = 0; e < DV; ++e) ref[e] = e < d ? fs.eref[off + 64 * e] : 0u;
+    for (int r = r0; r < nres; r += SPS * rs) {
+        F2 m[SPS][DV];
+        uint32_t me[SPS][DV];
+        F y[SPS];
+#pragma unroll
+        for (int j = 0; j < SPS; ++j) {
+            const auto S = FloodSlot::at<F>(scratch, slot_bytes, r + j * rs < nres ? r + j * rs : r, fs);
+            y[j] = S.yq[p];
 #pragma unroll
             for (int e = 0; e < DV; ++e)
-                if (e < d) {   // nlist order (:452-476)
-                    s0 += v0[e];
-                    s1 += v1[e];
+                if (e < d) {
+                    m[j][e] = S.m12[ref[e] >> 5];
+                    me[j][e] = S.meta[ref[e] >> 5];
                 }
-            S0.app[p] = s0;
-            if (two) S1.app[p] = s1;
+        }
+#pragma unroll
+        for (int j = 0; j < SPS; ++j) {
+            F sum = y[j];
+#pragma unroll
+            for (int e = 0; e < DV; ++e)
+                if (e < d) sum += flood_msg<F>(m[j][e], me[j][e], ref[e] & 31u);   // nlist order (:452-476)
+            if (r + j * rs < nres) FloodSlot::at<F>(scratch, slot_bytes, r + j * rs, fs).app[p] = sum;
         }
     }
 }
@@ -763,14 +845,34 @@ __global__ __launch_bounds__(256) void k_flood_account(DecodeArgs a, int b0, int
     if (a.frame_res) a.frame_res[b] = make_int4(w, uc, sf, 0);
 }
 
-// Resident codewords of the phase-per-launch flooding: their state fits the
-// Infinity Cache (LDPC_FLOOD_RESIDENT overrides).
-constexpr size_t kFloodPhaseExtra = 65536;   // per-slot counters after the slots (3 ints per slot)
-static int flood_phase_resident(size_t slot_bytes, size_t gscratch_bytes)
+// Messages between the phases: the packed row state (default) or the c2v
+// array (LDPC_FLOOD_MSG=c2v).
+static bool flood_packed()
 {
-    // 150 MB of state: 128 DVB-S2 codewords. At 192 MB (164) the rate fell by a
-    // fifth on some boxes and not on others -- the edge of what stays resident.
-    long k = (long)((150ull << 20) / slot_bytes);
+    const char *e = std::getenv("LDPC_FLOOD_MSG");
+    return !(e && std::strcmp(e, "c2v") == 0);
+}
+
+// Resident slots per step of the check (LDPC_FLOOD_SPS_CHECK) and bit
+// (LDPC_FLOOD_SPS_BIT) phase kernels.
+static int flood_sps(bool check)
+{
+    const char *e = std::getenv(check ? "LDPC_FLOOD_SPS_CHECK" : "LDPC_FLOOD_SPS_BIT");
+    if (e) return std::max(1, std::atoi(e));
+    return check || flood_packed() ? 1 : 2;   // packed bit phase: 1 (2 204 vs 2 124 Mbit/s fp32)
+}
+
+// Resident codewords of the phase-per-launch flooding: the state the phases
+// touch fits the Infinity Cache with room to spare. `touched` = bytes per slot
+// the phases read and write (the packed-message phases leave the c2v array of
+// the slot alone). Measured on DVB-S2 R1/2 with packed messages (4096
+// codewords, T=50): fp32 K = 96/112/128/144 -> 2277/2307/2331/2310 Mbit/s,
+// fp64 K = 64/80/96/128 -> 1520/1508/1487/1401 -- best near 110 MB touched.
+// LDPC_FLOOD_RESIDENT overrides.
+constexpr size_t kFloodPhaseExtra = 65536;   // per-slot counters after the slots (3 ints per slot)
+static int flood_phase_resident(size_t slot_bytes, size_t touched, size_t gscratch_bytes)
+{
+    long k = (long)((112ull << 20) / touched);
     if (const char *e = std::getenv("LDPC_FLOOD_RESIDENT")) k = std::atol(e);
     if (k > 4096) k = 4096;
     const long cap = (long)((gscratch_bytes - kFloodPhaseExtra) / slot_bytes);
@@ -812,12 +914,24 @@ struct FloodHalf {
         const dim3 cg((NPc + 255) / 256, (n + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW);
 #endif
         unsigned char *sc = scratch + sb * (size_t)lo;
-        if (fs->dc <= 8)
-            hipLaunchKernelGGL((k_flood_check<F, 8>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n);
-        else if (fs->dc <= 16)
-            hipLaunchKernelGGL((k_flood_check<F, 16>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n);
-        else
-            hipLaunchKernelGGL((k_flood_check<F, 32>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n);
+        const int sps = flood_sps(true);
+        const bool packed = flood_packed();
+#define CHK(DC, SPS)                                                                                     \
+    do {                                                                                                 \
+        if (packed) hipLaunchKernelGGL((k_flood_check<F, DC, SPS, false>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n); \
+        else hipLaunchKernelGGL((k_flood_check<F, DC, SPS, true>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n);         \
+    } while (0)
+        if (fs->dc <= 8) {
+            if (sps >= 4) CHK(8, 4);
+            else if (sps == 2) CHK(8, 2);
+            else CHK(8, 1);
+        } else if (fs->dc <= 16) {
+            if (sps >= 2) CHK(16, 2);
+            else CHK(16, 1);
+        } else {
+            CHK(32, 1);
+        }
+#undef CHK
     }
     void bit() const
     {
@@ -829,12 +943,27 @@ struct FloodHalf {
         const dim3 bg((NP + 255) / 256, (n + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW);
 #endif
         unsigned char *sc = scratch + sb * (size_t)lo;
-        if (fs->dv <= 8)
-            hipLaunchKernelGGL((k_flood_bit<F, 8>), bg, dim3(256), 0, s, *fs, sc, sb, n);
-        else if (fs->dv <= 16)
-            hipLaunchKernelGGL((k_flood_bit<F, 16>), bg, dim3(256), 0, s, *fs, sc, sb, n);
-        else
-            hipLaunchKernelGGL((k_flood_bit<F, 0>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+        const int sps = flood_sps(false);
+        if (flood_packed()) {
+            if (fs->dv <= 8) {
+                if (sps >= 2) hipLaunchKernelGGL((k_flood_bit_packed<F, 8, 2>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+                else hipLaunchKernelGGL((k_flood_bit_packed<F, 8, 1>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+            } else if (fs->dv <= 16) {
+                hipLaunchKernelGGL((k_flood_bit_packed<F, 16, 1>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+            } else {
+                hipLaunchKernelGGL((k_flood_bit_packed<F, 32, 1>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+            }
+            return;
+        }
+        if (fs->dv <= 8) {
+            if (sps >= 4) hipLaunchKernelGGL((k_flood_bit<F, 8, 4>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+            else hipLaunchKernelGGL((k_flood_bit<F, 8, 2>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+        } else if (fs->dv <= 16) {
+            if (sps >= 4) hipLaunchKernelGGL((k_flood_bit<F, 16, 4>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+            else hipLaunchKernelGGL((k_flood_bit<F, 16, 2>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+        } else {
+            hipLaunchKernelGGL((k_flood_bit<F, 0, 1>), bg, dim3(256), 0, s, *fs, sc, sb, n);
+        }
     }
     void end(int b0) const
     {
@@ -866,7 +995,8 @@ static hipError_t launch_flood_phase_t(const DevGraph &g, const FloodSched &fs, 
                                        const AuxStream *aux)
 {
     const size_t sb = kc.scratch_per_block;
-    const int K = flood_phase_resident(sb, gs_bytes);
+    const size_t c2v_bytes = (size_t)((fs.e_pad + 64 + 1) / 2 * 2) * sizeof(F);
+    const int K = flood_phase_resident(sb, flood_packed() ? sb - c2v_bytes : sb, gs_bytes);
     unsigned char *scratch = (unsigned char *)gs;
     int *unc = reinterpret_cast<int *>(scratch + sb * (size_t)K);   // per-slot counters after the slots
     int *wsum = unc + K, *ssum = wsum + K;

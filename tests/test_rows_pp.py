@@ -34,7 +34,12 @@ def test_pp_kernel_selected_for_the_bench_code(gpu_ctx_factory, monkeypatch):
     _kernel(monkeypatch, "fast")
     assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
     monkeypatch.delenv("LDPC_ROWS")
-    assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"      # the default
+    info = ctx.kernel_info(cfg)
+    assert info["kernel"] == "rows_pp"      # the default
+    # two slots of app[N+3] + c2v[e_pad+64] in one block per CU
+    assert info["blocks_per_cu"] == 1 and 2 * 8 * (ctx.graph.N + 3) < info["lds_bytes"] <= 160 * 1024
+    si = ctx.row_sched_info(cfg)
+    assert si["lds_bytes"] == info["lds_bytes"] and si["blocks_per_cu"] == 1
     # PEG 504x1008 has M <= 512: one row per thread, the one-codeword kernel
     assert gpu_ctx_factory("PEGReg504x1008.alist").kernel_info(cfg)["kernel"] == "rows_fast"
 
