@@ -18,7 +18,7 @@ struct NbDevGraph {
     const int32_t *col_ptr;       // [N + 1]
     const int32_t *col_slot;      // [E]      row-major slots of each symbol, nlist order
     const int32_t *col_pslot;     // [E]      the same edges as position-major slots k*M + j
-    const uint8_t *col_h;         // [E]      their coefficients
+    const uint8_t *col_h;         // [E]      their coefficients (low nibble) | slot XOR swizzle << 4 (nb.hip vn_lane)
     const uint8_t *gf_mul;        // [q * q]  multiplication table
     const uint8_t *gf_inv;        // [q]
 };
@@ -41,6 +41,10 @@ struct NbChoice {
     int lds_bytes = 0, threads = 0, dc = 0;
     size_t slot_bytes = 0;        // ems_global: message bytes per resident codeword
 };
+
+// Position-major message slot count (maxdc * M) padded to 2 mod 8: the row
+// stride of the chunk-major message layout (nb.hip).
+__host__ __device__ inline int nb_ep(const NbDevGraph &g) { return (g.maxdc * g.M + 5) / 8 * 8 + 2; }
 
 NbChoice nb_choose(const NbDevGraph &g, int maxdc);
 hipError_t nb_launch(const NbDevGraph &g, const NbArgs &a, const NbChoice &ch, void *scratch, int slots,

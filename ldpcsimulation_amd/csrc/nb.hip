@@ -29,6 +29,11 @@ namespace ldpc {
 
 constexpr float kInf = __builtin_huge_valf();
 
+// Symbol nodes of degree <= LDPC_EMS_VD keep their c2v in registers (0: re-read).
+#ifndef LDPC_EMS_VD
+#define LDPC_EMS_VD 4
+#endif
+
 // The graph, re-packed into LDS once per workgroup (global loads in the
 // per-iteration loops would put dependent L2 round trips on every round).
 // Edge slots are position-major: slot(j, k) = k*M + j for check j and mlist
@@ -188,7 +193,7 @@ __device__ __forceinline__ int gf16_xt(int v) { return ((v << 1) & 15) ^ ((v & 8
 // Entry a (symbol domain) of an edge's message lives at check-domain position
 // h*a. init: write v2c = L on every edge. Otherwise app = L + sum of the c2v
 // (nlist order), decision argmin app (first minimum), v2c = (app - c2v) - min.
-template <int Q, int MB>
+template <int Q, int MB, int VD>
 __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched &sc, const float *lam, uint8_t *dec,
                                         bool init)
 {
@@ -206,12 +211,19 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
     }
     const uint32_t vp = sc.vn[v];
     const int e0 = vp >> 8, e1 = e0 + (vp & 255);
+    // entry a of the edge: check-domain position h*a, stored at (h*a) ^ f, f = the
+    // slot's XOR swizzle (0 in the plain layout). A check node works on its stored
+    // vectors as they are: ECN(P shifted by f1, R shifted by f2) is ECN(P, R)
+    // shifted by f1 ^ f2 -- the same float sums, so the same minima -- and the
+    // host chooses f with the XOR over every check's slots = 0, so each output
+    // lands at exactly its own slot's swizzle. f spreads these gathers over the
+    // LDS banks (nb_api.cpp nb_swizzled_coefficients).
     auto addr = [&](int e, int (&ad)[Q]) {
-        const int s = sc.vslot[e], h1 = sc.vh[e];
+        const int s = sc.vslot[e], hv = sc.vh[e], h1 = hv & 15, f = hv >> 4;
         const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
 #pragma unroll
         for (int a = 0; a < Q; ++a) {
-            const int p = ((a & 1) ? h1 : 0) ^ ((a & 2) ? h2 : 0) ^ ((a & 4) ? h4 : 0) ^ ((a & 8) ? h8 : 0);
+            const int p = ((a & 1) ? h1 : 0) ^ ((a & 2) ? h2 : 0) ^ ((a & 4) ? h4 : 0) ^ ((a & 8) ? h8 : 0) ^ f;
             ad[a] = (((p >> 2) * Ep + s) << 2) + (p & 3);
         }
     };
@@ -222,6 +234,48 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
 #pragma unroll
             for (int a = 0; a < Q; ++a) msg[ad[a]] = app[a];
         }
+    } else if (VD > 0 && e1 - e0 <= VD) {
+        // degree <= VD: each c2v is read once and kept in registers with its
+        // addresses (the loop below re-reads and re-addresses every edge)
+        constexpr int K = VD > 0 ? VD : 1;
+        const int deg = e1 - e0;
+        float c[K][Q];
+        int ak[K][Q];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (k < deg) {
+                addr(e0 + k, ak[k]);
+#pragma unroll
+                for (int a = 0; a < Q; ++a) c[k][a] = msg[ak[k][a]];
+            }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (k < deg) {
+#pragma unroll
+                for (int a = 0; a < Q; ++a) app[a] += c[k][a];   // nlist order
+            }
+        int best = 0;
+        float bv = app[0];
+#pragma unroll
+        for (int a = 1; a < Q; ++a)
+            if (app[a] < bv) {
+                bv = app[a];
+                best = a;
+            }
+        dec[v] = (uint8_t)best;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (k < deg) {
+                float t[Q], mn = kInf;
+#pragma unroll
+                for (int a = 0; a < Q; ++a) {
+                    t[a] = app[a] - c[k][a];
+                    mn = fminf(mn, t[a]);
+                }
+#pragma unroll
+                for (int a = 0; a < Q; ++a) msg[ak[k][a]] = t[a] - mn;
+            }
+        return;
     } else {
         for (int e = e0; e < e1; ++e) {
             addr(e, ad);
@@ -295,7 +349,7 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     }
     __syncthreads();
     // ---- initial messages v2c = L (stored at the check-domain position h*x), decisions argmin L ----
-    for (int v = tid; v < N; v += nt) vn_lane<Q, MB>(msg, Ep, v, sc, lam, dec, true);
+    for (int v = tid; v < N; v += nt) vn_lane<Q, MB, 0>(msg, Ep, v, sc, lam, dec, true);
     __syncthreads();
     int fail = syndrome_fail<Q>(g, sc, dec, gmul);
     int it = 0;
@@ -325,7 +379,7 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         }
         __syncthreads();
         // ---- symbol nodes: lane x = variable-domain symbol, reads c2v(x) at position h*x ----
-        for (int v = tid; v < N; v += nt) vn_lane<Q, MB>(msg, Ep, v, sc, lam, dec, false);
+        for (int v = tid; v < N; v += nt) vn_lane<Q, MB, LDPC_EMS_VD>(msg, Ep, v, sc, lam, dec, false);
         __syncthreads();
         fail = syndrome_fail<Q>(g, sc, dec, gmul);
         ++it;
@@ -356,8 +410,6 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// Position-major slot count (maxdc * M) padded to 2 mod 8.
-__host__ __device__ inline int nb_ep(const NbDevGraph &g) { return (g.maxdc * g.M + 5) / 8 * 8 + 2; }
 
 // dynamic LDS: [msg 16*Ep f32 (ems_lds only)] [lam N*m f32] [dec N u8] [gf_mul Q*Q u8] [cn_d M u8]
 //              [ecol Ms u16] [eh Ms u8] [vn N u32] [vslot E u16] [vh E u8]

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -114,7 +115,84 @@ struct ldpc_nb_ctx {
     Buf graph, counts, y_stage, c_stage, d_stage, fr_stage, scratch;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
+    const uint8_t *col_h_swz = nullptr;   // device: col_h with the slot swizzles (nb_swizzled_coefficients)
 };
+
+// LDPC_EMS_SWIZZLE=0 keeps the plain message layout (A/B).
+static bool nb_swizzle_enabled()
+{
+    const char *e = std::getenv("LDPC_EMS_SWIZZLE");
+    return !(e && std::atoi(e) == 0);
+}
+
+// XOR swizzles of the message slots for the symbol-node gathers of nb.hip
+// (vn_lane: entry a of an edge is read at check-domain position (h*a) ^ f,
+// one ds_read_b32 per entry, the lanes of a wave on consecutive symbols).
+// Those gathers hit random banks in the plain layout (f = 0): 3.7 LDS cycles
+// per 32-lane group against 1 conflict-free (GF(16) N=1000 code). A local
+// search picks f per slot under the constraint that the XOR of f over every
+// check's slots is 0 (what keeps the check node's outputs in place), scoring
+// the LDS bank model of the gathers: two groups of 32 lanes, bank = dword mod
+// 32, cost = the most-used bank. Moves XOR the same delta into two slots of one
+// check. Deterministic (fixed seed). Returned: col_h | f << 4 per column entry.
+static std::vector<uint8_t> nb_swizzled_coefficients(const ldpc_nb_graph &g, const std::vector<int32_t> &pslot,
+                                                     const std::vector<uint8_t> &colh, const std::vector<uint8_t> &mul)
+{
+    std::vector<uint8_t> out(colh);
+    if (g.q != ldpc::kNbQ || g.E == 0) return out;
+    const int Q = g.q, N = g.N, M = g.M, DV = std::max(g.maxdv, 1);
+    const int Ep = (g.maxdc * g.M + 5) / 8 * 8 + 2;   // nb_ep
+    std::vector<uint8_t> f((size_t)g.maxdc * M, 0);
+    std::vector<int> slot_v(f.size(), -1), slot_k(f.size(), 0);
+    for (int v = 0; v < N; ++v)
+        for (int e = g.col_ptr[v]; e < g.col_ptr[v + 1]; ++e) {
+            slot_v[pslot[e]] = v;
+            slot_k[pslot[e]] = e - g.col_ptr[v];
+        }
+    auto gcost = [&](int grp, int k) {   // summed over the Q entries of edge index k of a 32-symbol group
+        int tot = 0;
+        for (int a = 0; a < Q; ++a) {
+            int cnt[32] = {0}, mx = 0;
+            for (int v = grp * 32; v < std::min(N, grp * 32 + 32); ++v) {
+                const int e = g.col_ptr[v] + k;
+                if (e >= g.col_ptr[v + 1]) continue;
+                const int sl = pslot[e], p = mul[(size_t)colh[e] * Q + a] ^ f[sl];
+                mx = std::max(mx, ++cnt[(((p >> 2) * Ep + sl) * 4 + (p & 3)) & 31]);
+            }
+            tot += mx;
+        }
+        return tot;
+    };
+    const int ngroups = (N + 31) / 32;
+    std::vector<int> C((size_t)ngroups * DV);
+    for (int grp = 0; grp < ngroups; ++grp)
+        for (int k = 0; k < DV; ++k) C[(size_t)grp * DV + k] = gcost(grp, k);
+    uint32_t x = 0x9e3779b9u;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 17; x ^= x << 5; return x; };
+    const long moves = std::min(200000L, 40L * g.E);
+    for (long it = 0; it < moves; ++it) {
+        const int j = (int)(rnd() % (uint32_t)M), d = g.row_ptr[j + 1] - g.row_ptr[j];
+        const int k1 = (int)(rnd() % (uint32_t)d);
+        int k2 = (int)(rnd() % (uint32_t)(d - 1));
+        if (k2 >= k1) ++k2;
+        const uint8_t delta = (uint8_t)(1 + rnd() % (uint32_t)(Q - 1));
+        const int s1 = k1 * M + j, s2 = k2 * M + j;
+        const int a1 = (slot_v[s1] / 32) * DV + slot_k[s1], a2 = (slot_v[s2] / 32) * DV + slot_k[s2];
+        const int before = C[a1] + (a2 != a1 ? C[a2] : 0);
+        f[s1] ^= delta;
+        f[s2] ^= delta;
+        const int n1 = gcost(a1 / DV, a1 % DV), n2 = a2 != a1 ? gcost(a2 / DV, a2 % DV) : 0;
+        if (n1 + n2 <= before) {
+            C[a1] = n1;
+            if (a2 != a1) C[a2] = n2;
+        } else {
+            f[s1] ^= delta;
+            f[s2] ^= delta;
+        }
+    }
+    for (int e = 0; e < g.E; ++e) out[e] = (uint8_t)(colh[e] | (f[pslot[e]] << 4));
+    return out;
+}
 
 // Build the CSR views from (row, value) lists per column and (column, value) per row (0-based).
 static int build_nb(int N, int M, int q, const std::vector<std::vector<std::pair<int, int>>> &cols,
@@ -303,7 +381,8 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
                     pslot[e] = (r - g->row_ptr[j]) * g->M + j;
                     colh[e] = g->row_h[r];
                 }
-    const size_t total = n_rp + n_rc + n_cp + 2 * n_cs + 2 * (size_t)g->E + mul.size() + inv.size() + 256;
+    const std::vector<uint8_t> colhs = nb_swizzled_coefficients(*g, pslot, colh, mul);
+    const size_t total = n_rp + n_rc + n_cp + 2 * n_cs + 3 * (size_t)g->E + mul.size() + inv.size() + 256;
     std::vector<uint8_t> blob(total, 0);
     size_t off = 0;
     auto put = [&](const void *src, size_t n) {
@@ -317,7 +396,7 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
                  o_cp = put(g->col_ptr.data(), n_cp), o_cs = put(g->col_slot.data(), n_cs),
                  o_h = put(g->row_h.data(), g->E), o_mul = put(mul.data(), mul.size()),
                  o_inv = put(inv.data(), inv.size()), o_ps = put(pslot.data(), n_cs),
-                 o_ch = put(colh.data(), g->E);
+                 o_ch = put(colh.data(), g->E), o_chs = put(colhs.data(), g->E);
     NB_HIP_TRY(c->graph.ensure(off));
     NB_HIP_TRY(hipMemcpy(c->graph.p, blob.data(), off, hipMemcpyHostToDevice));
     auto *base = (uint8_t *)c->graph.p;
@@ -335,6 +414,7 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
     c->dg.gf_inv = base + o_inv;
     c->dg.col_pslot = (const int32_t *)(base + o_ps);
     c->dg.col_h = base + o_ch;
+    c->col_h_swz = base + o_chs;
     c->dg.maxdc = g->maxdc;
     if (!ldpc::nb_choose(c->dg, g->maxdc).name[0]) {
         ldpc_nb_ctx_destroy(c);
@@ -404,7 +484,11 @@ static int run(ldpc_nb_ctx *c, const ldpc::NbArgs &a)
         NB_HIP_TRY(c->scratch.ensure(ch.slot_bytes * (size_t)slots));
     }
     NB_HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    NB_HIP_TRY(ldpc::nb_launch(c->dg, a, ch, c->scratch.p, slots, c->num_cus, c->stream));
+    ldpc::NbDevGraph dg = c->dg;
+    // untruncated messages (nm >= q): the XOR-swizzled layout; truncation ranks
+    // entries by symbol on ties, so it keeps the plain one (nb.hip vn_lane)
+    if (a.nm >= dg.q && nb_swizzle_enabled()) dg.col_h = c->col_h_swz;
+    NB_HIP_TRY(ldpc::nb_launch(dg, a, ch, c->scratch.p, slots, c->num_cus, c->stream));
     NB_HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
     return LDPC_OK;
