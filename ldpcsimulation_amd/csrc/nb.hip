@@ -29,9 +29,14 @@ namespace ldpc {
 
 constexpr float kInf = __builtin_huge_valf();
 
+// Timing-only ablations (wrong results): 1 = no check nodes, 2 = no symbol
+// nodes, 3 = no per-iteration syndrome (run with early stop off).
+#ifndef LDPC_EMS_EXP
+#define LDPC_EMS_EXP 0
+#endif
 // Symbol nodes of degree <= LDPC_EMS_VD keep their c2v in registers (0: re-read).
 #ifndef LDPC_EMS_VD
-#define LDPC_EMS_VD 4
+#define LDPC_EMS_VD 2
 #endif
 
 // The graph, re-packed into LDS once per workgroup (global loads in the
@@ -52,6 +57,9 @@ struct NbSched {
     const uint8_t *vh;       // [E]    their coefficients
 };
 
+// GF(16) (x^4 + x + 1): v * x.
+__device__ __forceinline__ int gf16_xt(int v) { return ((v << 1) & 15) ^ ((v & 8) ? 3 : 0); }
+
 template <int Q>
 __device__ __forceinline__ int syndrome_fail(const NbDevGraph &g, const NbSched &s, const uint8_t *dec,
                                              const uint8_t *gmul)
@@ -62,7 +70,13 @@ __device__ __forceinline__ int syndrome_fail(const NbDevGraph &g, const NbSched 
         int sy = 0;
         for (int k = 0; k < d; ++k) {
             const int sl = k * g.M + j;
-            sy ^= gmul[s.eh[sl] * Q + dec[s.ecol[sl]]];
+            if (Q == 16) {   // h * dec by xtime in registers (one LDS round trip less than the table)
+                const int h1 = s.eh[sl], x = dec[s.ecol[sl]];
+                const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
+                sy ^= ((x & 1) ? h1 : 0) ^ ((x & 2) ? h2 : 0) ^ ((x & 4) ? h4 : 0) ^ ((x & 8) ? h8 : 0);
+            } else {
+                sy ^= gmul[s.eh[sl] * Q + dec[s.ecol[sl]]];
+            }
         }
         fail |= sy != 0;
     }
@@ -185,9 +199,8 @@ __device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int di
     store_out<Q>(msg, Ep, slot(D - 1), F[D - 2], nm, offset);
 }
 
-// GF(16) products h*a for a = 0..15 (x^4 + x + 1): h*2^i by xtime, then the
-// xor of the powers in a.
-__device__ __forceinline__ int gf16_xt(int v) { return ((v << 1) & 15) ^ ((v & 8) ? 3 : 0); }
+// GF(16) products h*a for a = 0..15: h*2^i by xtime (gf16_xt), then the xor of
+// the powers in a.
 
 // ---- symbol node: one lane per symbol, the 16-entry vectors in registers ----
 // Entry a (symbol domain) of an edge's message lives at check-domain position
@@ -359,7 +372,7 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     const int cj0 = (tid >> 6) * 32 + (tid & 31);
     while (it < a.T && (!a.early_stop || fail)) {
         // ---- check nodes ----
-        for (int j = cj0; j < M; j += cpr) {
+        for (int j = cj0; j < M && LDPC_EMS_EXP != 1; j += cpr) {
             switch (sc.cn_d[j]) {
             case 2: cn_lane<Q, 2>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
             case 3: cn_lane<Q, 3>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
@@ -379,9 +392,10 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         }
         __syncthreads();
         // ---- symbol nodes: lane x = variable-domain symbol, reads c2v(x) at position h*x ----
-        for (int v = tid; v < N; v += nt) vn_lane<Q, MB, LDPC_EMS_VD>(msg, Ep, v, sc, lam, dec, false);
+        for (int v = tid; v < N && LDPC_EMS_EXP != 2; v += nt)
+            vn_lane<Q, MB, LDPC_EMS_VD>(msg, Ep, v, sc, lam, dec, false);
         __syncthreads();
-        fail = syndrome_fail<Q>(g, sc, dec, gmul);
+        if (LDPC_EMS_EXP != 3) fail = syndrome_fail<Q>(g, sc, dec, gmul);
         ++it;
     }
 
@@ -480,14 +494,15 @@ NbChoice nb_choose(const NbDevGraph &g, int maxdc)
 {
     NbChoice ch;
     ch.dc = maxdc <= 4 ? 4 : 8;
-    // 512 threads: the register-resident check node needs up to ~180 VGPRs
-    // (1024-thread blocks cap a wave at 128 and spill); LDS allows one
-    // workgroup per CU either way. LDPC_EMS_THREADS=1024 selects the other
-    // build for DC = 4 (A/B only).
+    // DC = 4: 1024 threads (4 waves per SIMD; 128 VGPRs, spills only around
+    // the codeword loop: 8.12 vs 8.00 Gbit/s at 2.0 dB with 512),
+    // LDPC_EMS_THREADS=512 the other build. DC = 8: 512 (its check node needs
+    // ~180 VGPRs). LDS allows one workgroup per CU either way.
     ch.threads = 512;
     if (ch.dc == 4) {
+        ch.threads = 1024;
         const char *e = std::getenv("LDPC_EMS_THREADS");
-        if (e && std::atoi(e) == 1024) ch.threads = 1024;
+        if (e && std::atoi(e) == 512) ch.threads = 512;
     }
     const size_t aux = aux_bytes(g), msgb = align16((size_t)nb_ep(g) * g.q * 4);
     if (maxdc > kNbMaxDc || aux > kNbMaxLds || nb_ep(g) > 65535 || g.N > 65535) {

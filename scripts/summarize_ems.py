@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Summarise scripts/profile_ems.sh output: per-full-launch PMC of the EMS
+kernel (the warm-up launch of 1 024 codewords is dropped: dispatches whose
+GRBM_GUI_ACTIVE is below half the largest), kernel-trace average and the
+derived rates. Usage: summarize_ems.py SRC_DIR OUT_JSON NOTE"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main(src, out, note=""):
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = set()
+    for f in glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "k_ems" in r["Kernel_Name"]:
+                names.add(r["Kernel_Name"])
+                per[(f.split(os.sep)[-2] if False else os.path.relpath(f, src).split(os.sep)[0], r["Dispatch_Id"])][
+                    r["Counter_Name"]] += float(r["Counter_Value"])
+    # full launches: per pass, keep dispatches with the largest activity
+    passes = collections.defaultdict(list)
+    for (p, d), c in per.items():
+        passes[p].append(c)
+    pmc = {}
+    for p, lst in passes.items():
+        key = max(lst[0], key=lambda k: 0)  # any counter of the pass
+        big = max(sum(c.values()) for c in lst)
+        full = [c for c in lst if sum(c.values()) >= 0.5 * big]
+        for k in full[0]:
+            pmc[k] = sum(c[k] for c in full) / len(full)
+    st = list(csv.DictReader(open(glob.glob(os.path.join(src, "stats", "**", "*kernel_stats.csv"), recursive=True)[0])))
+    ems = [r for r in st if "k_ems" in r["Name"]]
+    d = {}
+    cyc = pmc.get("GRBM_GUI_ACTIVE")
+    if cyc:
+        d["cycles_per_launch"] = cyc / 8   # GRBM_GUI_ACTIVE sums the 8 XCDs
+        if "SQ_INSTS_VALU" in pmc:
+            d["valu_per_cu_cycle"] = pmc["SQ_INSTS_VALU"] / 256 / d["cycles_per_launch"]
+        if "SQ_INSTS_LDS" in pmc:
+            d["lds_instr_per_cu_cycle"] = pmc["SQ_INSTS_LDS"] / 256 / d["cycles_per_launch"]
+    if "SQ_WAIT_ANY" in pmc and "SQ_WAVE_CYCLES" in pmc:
+        d["wait_any_frac"] = pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
+    if "SQ_LDS_BANK_CONFLICT" in pmc and "SQ_INSTS_LDS" in pmc:
+        d["bank_conflict_cycles_per_lds_instr"] = pmc["SQ_LDS_BANK_CONFLICT"] / pmc["SQ_INSTS_LDS"]
+    if "SQ_ACTIVE_INST_VALU" in pmc and "SQ_WAVE_CYCLES" in pmc:
+        d["active_valu_frac_of_wave_cycles"] = pmc["SQ_ACTIVE_INST_VALU"] / pmc["SQ_WAVE_CYCLES"]
+    res = {"source": f"{src} (scripts/profile_ems.sh)", "kernels": sorted(names),
+           "kernel_trace": [{k: r[k] for k in ("Name", "Calls", "AverageNs")} for r in ems],
+           "pmc_per_full_launch": pmc, "derived": d, "note": note}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res["derived"], indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
