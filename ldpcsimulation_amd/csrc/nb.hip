@@ -29,6 +29,10 @@ namespace ldpc {
 
 constexpr float kInf = __builtin_huge_valf();
 
+// Check-lane addresses recomputed per iteration (1) or hoisted by the compiler (0).
+#ifndef LDPC_EMS_OPAQUE
+#define LDPC_EMS_OPAQUE 1
+#endif
 // Timing-only ablations (wrong results): 1 = no check nodes, 2 = no symbol
 // nodes, 3 = no per-iteration syndrome (run with early stop off).
 #ifndef LDPC_EMS_EXP
@@ -372,7 +376,12 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     const int cj0 = (tid >> 6) * 32 + (tid & 31);
     while (it < a.T && (!a.early_stop || fail)) {
         // ---- check nodes ----
-        for (int j = cj0; j < M && LDPC_EMS_EXP != 1; j += cpr) {
+        // the lane's first check, opaque per iteration: its message addresses are
+        // recomputed here (a few VALU) instead of being hoisted out of the
+        // iteration loop and, at 128 VGPRs, spilled and reloaded every iteration
+        int cj = cj0;
+        if (LDPC_EMS_OPAQUE) asm volatile("" : "+v"(cj));
+        for (int j = cj; j < M && LDPC_EMS_EXP != 1; j += cpr) {
             switch (sc.cn_d[j]) {
             case 2: cn_lane<Q, 2>(msg, Ep, M, j, cdir, a.nm, a.offset); break;
             case 3: cn_lane<Q, 3>(msg, Ep, M, j, cdir, a.nm, a.offset); break;

@@ -4,10 +4,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${RUN_TAG:-r03p22}; mkdir -p $O
 for r in 1 2; do
-  for arm in default noshift t512; do
+  for arm in default noopq t512; do
     unset LDPC_LIB LDPC_EMS_THREADS
     case $arm in
-      noshift) export LDPC_LIB=emsnoshift;;
+      noopq) export LDPC_LIB=emsnoopq;;
       t512) export LDPC_EMS_THREADS=512;;
     esac
     timeout -k 10 200 python3 scripts/bench_ems.py --ebn0 1.5 2.0 --steps 3 > $O/$arm-$r.jsonl 2> $O/$arm-$r.err || { tail -5 $O/$arm-$r.err; exit 1; }

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Summarise scripts/profile_ems.sh output: per-full-launch PMC of the EMS
-kernel (the warm-up launch of 1 024 codewords is dropped: dispatches whose
-GRBM_GUI_ACTIVE is below half the largest), kernel-trace average and the
-derived rates. Usage: summarize_ems.py SRC_DIR OUT_JSON NOTE"""
+"""Summarise a directory of rocprofv3 PMC passes (p1, p2, ... as written by
+scripts/profile_ems.sh or scripts/pmc_layered.sh): per-full-launch counters of
+the kernel whose name contains PATTERN (dispatches whose counters sum to less
+than half the largest of their pass -- warm-up launches -- are dropped), the
+kernel-trace average when a stats/ run exists, and derived rates.
+Usage: summarize_pmc.py SRC_DIR OUT_JSON PATTERN [NOTE]"""
 import collections
 import csv
 import glob
@@ -11,12 +13,12 @@ import os
 import sys
 
 
-def main(src, out, note=""):
+def main(src, out, pattern="k_ems", note=""):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = set()
     for f in glob.glob(os.path.join(src, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_ems" in r["Kernel_Name"]:
+            if pattern in r["Kernel_Name"]:
                 names.add(r["Kernel_Name"])
                 per[(f.split(os.sep)[-2] if False else os.path.relpath(f, src).split(os.sep)[0], r["Dispatch_Id"])][
                     r["Counter_Name"]] += float(r["Counter_Value"])
@@ -31,8 +33,8 @@ def main(src, out, note=""):
         full = [c for c in lst if sum(c.values()) >= 0.5 * big]
         for k in full[0]:
             pmc[k] = sum(c[k] for c in full) / len(full)
-    st = list(csv.DictReader(open(glob.glob(os.path.join(src, "stats", "**", "*kernel_stats.csv"), recursive=True)[0])))
-    ems = [r for r in st if "k_ems" in r["Name"]]
+    sf = glob.glob(os.path.join(src, "stats", "**", "*kernel_stats.csv"), recursive=True)
+    ems = [r for r in csv.DictReader(open(sf[0])) if pattern in r["Name"]] if sf else []
     d = {}
     cyc = pmc.get("GRBM_GUI_ACTIVE")
     if cyc:
@@ -45,9 +47,13 @@ def main(src, out, note=""):
         d["wait_any_frac"] = pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
     if "SQ_LDS_BANK_CONFLICT" in pmc and "SQ_INSTS_LDS" in pmc:
         d["bank_conflict_cycles_per_lds_instr"] = pmc["SQ_LDS_BANK_CONFLICT"] / pmc["SQ_INSTS_LDS"]
+    if "TCC_HIT_sum" in pmc and "TCC_MISS_sum" in pmc:
+        d["l2_hit_rate"] = pmc["TCC_HIT_sum"] / max(1.0, pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"])
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:   # KiB; gfx950 FETCH_SIZE counts wide reads at half (MI355X_MICROARCH)
+        d["hbm_bytes_upper"] = (2 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024
     if "SQ_ACTIVE_INST_VALU" in pmc and "SQ_WAVE_CYCLES" in pmc:
         d["active_valu_frac_of_wave_cycles"] = pmc["SQ_ACTIVE_INST_VALU"] / pmc["SQ_WAVE_CYCLES"]
-    res = {"source": f"{src} (scripts/profile_ems.sh)", "kernels": sorted(names),
+    res = {"source": src, "kernels": sorted(names),
            "kernel_trace": [{k: r[k] for k in ("Name", "Calls", "AverageNs")} for r in ems],
            "pmc_per_full_launch": pmc, "derived": d, "note": note}
     json.dump(res, open(out, "w"), indent=1)
