@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 8
+#define LDPC_ABI_VERSION 9
 
 typedef enum {
     LDPC_OK = 0,
@@ -125,7 +125,7 @@ typedef struct {
 
 int         ldpc_abi_version(void);
 const char *ldpc_last_error(void);
-/* 1 when the fp64 NMS division m / alpha (applyNormalization,
+/* (ABI 9) 1 when the fp64 NMS division m / alpha (applyNormalization,
  * decodeMinSum.cpp:494-499) runs as Markstein's q = m*r, q += fma(-q, alpha, m)*r
  * with r = RN(1/alpha) -- exact for alpha = P * 2^E, odd P < 2^20, 2^-900 < alpha
  * <= 2^60 -- else 0 (IEEE division). No device call. */

@@ -22,7 +22,7 @@ LDPC_OK = 0
 MS, NMS, OMS, BP = 0, 1, 2, 3
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 8
+ABI_VERSION = 9
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
