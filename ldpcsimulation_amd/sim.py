@@ -104,7 +104,7 @@ class _Comm:
 
     def _tensor(self, arr: np.ndarray):
         import torch
-        t = torch.from_numpy(np.ascontiguousarray(arr))
+        t = torch.from_numpy(np.array(arr, copy=True))   # a copy: the collective works in place
         if self.dist.get_backend() == "nccl":
             t = t.to(self.device if self.device is not None else "cuda")
         return t
@@ -126,6 +126,19 @@ class _Comm:
         return np.concatenate([o.cpu().numpy() for o in out])
 
 
+@dataclass
+class PointState:
+    """An SNR point after its fully counted rounds: what a checkpoint holds
+    (checkpoint.py). Frames are keyed by global index, so decoding on from
+    next_frame with these totals reproduces the uninterrupted run exactly, for
+    any number of ranks and round sizes."""
+    next_frame: int                 # first global frame not yet counted
+    acc: np.ndarray                 # the six counters (COUNT_KEYS order)
+    hist: np.ndarray                # error-weight histogram over all ranks
+    rounds: int = 0
+    frames_decoded: int = 0
+
+
 def round_sizes(batch: int, first_round: Optional[int] = None):
     """Frames per rank of rounds 0, 1, 2, ...: first_round (default min(batch, 1024)),
     doubling up to batch. A low-SNR point stops near its 40th frame error after a
@@ -140,7 +153,9 @@ def round_sizes(batch: int, first_round: Optional[int] = None):
 def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, ebn0_db: float,
                    batch: int, min_bit_err: int = 200, min_frame_err: int = 40,
                    max_frames: Optional[int] = None, exact_stop: bool = True, device=None,
-                   iters_in_frames: bool = False, launcher=None, first_round: Optional[int] = None) -> PointResult:
+                   iters_in_frames: bool = False, launcher=None, first_round: Optional[int] = None,
+                   resume: Optional[PointState] = None,
+                   on_round: Optional[Callable[[PointState], None]] = None) -> PointResult:
     """Run one SNR point to the reference's stop rule.
 
     run_batch(first_cw, n) must decode global frames first_cw..first_cw+n-1 on
@@ -157,18 +172,30 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
     counts show that at least two more rounds are needed, round k+1 is launched
     before round k is reduced, so the host-side reduction and the all-reduce
     overlap the next decode. The results are the same: frames are keyed by
-    global index and a round launched ahead of the stop is discarded."""
+    global index and a round launched ahead of the stop is discarded.
+
+    resume: start from a checkpointed PointState (the same on every rank) instead
+    of frame 0. on_round(state): called on every rank after each fully counted
+    round with the point's state (its histogram all-reduced: a collective), for
+    checkpoints."""
     comm = _Comm(device)
     acc = np.zeros(6, dtype=np.int64)
     res = PointResult(ebn0_db, N, T)
     hist_local = np.zeros(N, dtype=np.int64)   # rounds fully counted: this rank's frames
     hist_cut = np.zeros(N, dtype=np.int64)     # the cut round: all ranks' frames (gathered)
+    hist_base = np.zeros(N, dtype=np.int64)    # resumed rounds: all ranks' frames
     rnd = 0
     ahead = False          # round rnd already launched (into slot rnd % 2)
     last = None            # the previous round's all-reduced increments
     sizes, starts = [], [0]    # frames per rank of each round; global first frame of each round
     gen = round_sizes(batch, first_round)
     decoded = 0
+    rounds0 = 0
+    if resume is not None:
+        acc = np.asarray(resume.acc, dtype=np.int64).copy()
+        hist_base = np.asarray(resume.hist, dtype=np.int64).copy()
+        starts = [int(resume.next_frame)]
+        decoded, rounds0 = int(resume.frames_decoded), int(resume.rounds)
 
     def size_of(r):
         while len(sizes) <= r:
@@ -221,12 +248,15 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
             acc = after
             w = raw[:, 0]
             np.add.at(hist_local, w[w > 0] - 1, 1)
+            if on_round is not None:
+                on_round(PointState(starts[rnd] + size_of(rnd) * comm.world, acc.copy(),
+                                    comm.allreduce_sum(hist_local) + hist_base, rounds0 + rnd + 1, decoded))
         rnd += 1
     if launcher is not None and ahead:
         decoded += len(launcher.collect(rnd % 2)) * comm.world   # drain the round launched past the stop
-    hist = comm.allreduce_sum(hist_local) + hist_cut
+    hist = comm.allreduce_sum(hist_local) + hist_cut + hist_base
     res.counts = dict(zip(COUNT_KEYS, (int(x) for x in acc)))
-    res.rounds = rnd
+    res.rounds = rounds0 + rnd
     res.frames_decoded = decoded
     res.hist = hist
     return res

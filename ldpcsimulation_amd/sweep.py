@@ -20,6 +20,11 @@ line for each point.
     python -m ldpcsimulation_amd.sweep codes/gf16_N1000_dv2_dc4.alist --ems --rate 0.5 --snr 1.5 2.0 -T 20
 Log line: SNR BER avgIt FER T [Ymax] [alpha] [delta] alist (EMS: SNR BER avgIt FER T nm offset alist;
 BER over coded bits, 4 per GF(16) symbol).
+
+--checkpoint FILE appends each point's running totals after every round
+(checkpoint.py); a sweep restarted with the same FILE and settings takes the
+seed from it, skips finished points and resumes the others at their next
+frame, with the totals an uninterrupted run gives.
 """
 from __future__ import annotations
 
@@ -29,7 +34,7 @@ import os
 import sys
 import time
 
-from . import native, sim
+from . import checkpoint, native, sim
 
 VARIANTS = {"ms": native.MS, "nms": native.NMS, "oms": native.OMS, "bp": native.BP}
 
@@ -72,7 +77,46 @@ def parse(argv=None):
                    help="collective backend for world > 1 (nccl = RCCL over xGMI; gloo: CPU tensors)")
     p.add_argument("--share-device", action="store_true",
                    help="every rank on device 0 (rehearsal of N ranks on one GPU, with --backend gloo)")
+    p.add_argument("--checkpoint", metavar="FILE",
+                   help="per-round progress file (.partial); an existing one is resumed (same settings)")
     return p.parse_args(argv)
+
+
+def _checkpoint_config(a) -> dict:
+    """Every setting that changes a point's result (not the batch or round sizes,
+    the GPU count or the log options: exact_stop makes totals independent of them)."""
+    return {"alist": os.path.basename(a.alist), "alist_md5": checkpoint.file_digest(a.alist), "rate": a.rate,
+            "snr": list(a.snr), "T": a.iterations, "variant": a.variant, "alpha": a.alpha, "delta": a.delta,
+            "quantize": a.quantize, "saturate": a.saturate, "precision": a.precision, "schedule": a.schedule,
+            "min_bit_errors": a.min_bit_errors, "min_frame_errors": a.min_frame_errors, "max_frames": a.max_frames,
+            "codewords_md5": checkpoint.file_digest(a.codewords), "ems": a.ems, "nm": a.nm, "offset": a.offset,
+            "early_stop": not a.no_early_stop}
+
+
+def _run_points(a, ck, rank, n_hist, run_point):
+    """run_point(k, snr, resume, on_round) -> (result, log line, json dict) for each
+    point not finished in the checkpoint; rank 0 logs and records each point.
+    n_hist: the points' histogram length (bits per frame)."""
+    for k, snr in enumerate(a.snr):
+        done = ck.done_line(k, snr) if ck else None
+        if done is not None:
+            if rank == 0:
+                print(done, flush=True)   # appended to the log by the run that finished it
+            continue
+        resume = ck.point_state(k, snr, n_hist) if ck else None
+        on_round = (lambda st, k=k, snr=snr: ck.save_round(k, snr, st)) if ck else None
+        res, line, js = run_point(k, snr, resume, on_round)
+        if rank == 0:
+            if a.log:
+                with open(a.log, "a") as f:
+                    f.write(line + "\n")
+            print(line, flush=True)
+            if a.json:
+                js["resumed_from_frame"] = resume.next_frame if resume else 0
+                print(json.dumps(js), flush=True)
+        if ck:
+            ck.save_done(k, snr, line)
+
 
 
 def main(argv=None) -> int:
@@ -89,6 +133,11 @@ def main(argv=None) -> int:
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
+    ck = checkpoint.SweepCheckpoint(a.checkpoint, _checkpoint_config(a), writer=rank == 0) if a.checkpoint else None
+    if ck and ck.seed is not None:
+        if a.seed is not None and a.seed != ck.seed:
+            raise checkpoint.CheckpointMismatch(f"--seed {a.seed} != the checkpoint's seed {ck.seed}")
+        a.seed = ck.seed          # every rank read the same file
     seed = a.seed if a.seed is not None else int(time.time())
     if world > 1 and a.seed is None:
         # every rank must key its noise with rank 0's seed (ranks may start in different seconds)
@@ -99,8 +148,10 @@ def main(argv=None) -> int:
         seed = int(t.item())
     if os.environ.get("LDPC_SWEEP_REPORT_SEED"):   # tests: every rank reports the seed it keys its noise with
         print(json.dumps({"rank": rank, "seed": seed}), file=sys.stderr, flush=True)
+    if ck:
+        ck.start(seed)
     if a.ems:
-        return _ems_sweep(a, seed, world, rank, device)
+        return _ems_sweep(a, seed, world, rank, device, ck)
     cfg = native.DecoderConfig(variant=VARIANTS[a.variant], T=a.iterations, alpha=a.alpha, delta=a.delta,
                                precision=native.F64 if a.precision == "f64" else native.F32,
                                schedule=native.LAYERED if a.schedule == "layered" else native.FLOODING)
@@ -123,70 +174,61 @@ def main(argv=None) -> int:
     if a.codewords:
         from .codes import read_codeword_file
         ctx.set_codewords(read_codeword_file(a.codewords, g.N))
-    for k, snr in enumerate(a.snr):
-        def run_batch(first, n, snr=snr, k=k):
+    def run_point(k, snr, resume, on_round):
+        def run_batch(first, n):
             fr, _ = ctx.sim_batch(snr, a.rate, cfg, seed, k, first, n)
             return fr
 
         launcher = None
         if not a.sync:
             # rounds run ahead: round k+1 decodes while round k is reduced (sim.AsyncLauncher)
-            def run_launch(first, n, frames_dev, snr=snr, k=k):
+            def run_launch(first, n, frames_dev):
                 ctx.sim_launch(snr, a.rate, cfg, seed, k, first, n, frames_dev)
             launcher = sim.AsyncLauncher(ctx, a.batch, run_launch)
         t0 = time.perf_counter()
         res = sim.simulate_point(run_batch, g.N, a.iterations, snr, a.batch, a.min_bit_errors,
-                                 min_fe, a.max_frames, device=device, launcher=launcher, first_round=a.first_round)
+                                 min_fe, a.max_frames, device=device, launcher=launcher, first_round=a.first_round,
+                                 resume=resume, on_round=on_round)
         dt = time.perf_counter() - t0
-        if rank == 0:
-            line = res.log_line(a.alist, extra)
-            if a.log:
-                with open(a.log, "a") as f:
-                    f.write(line + "\n")
-            print(line, flush=True)
-            if a.json:
-                c = res.counts
-                print(json.dumps({"ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "seconds": dt,
-                                  "mbit_s": c["frames"] * g.N / dt / 1e6 if dt > 0 else None,
-                                  "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
-                                  "precision": a.precision, "schedule": a.schedule, "variant": a.variant,
-                                  "kernel": ctx.kernel_info(cfg)["kernel"], "rounds": res.rounds,
-                                  "frames_decoded": res.frames_decoded}),
-                      flush=True)
+        c = res.counts
+        return res, res.log_line(a.alist, extra), {
+            "ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "seconds": dt,
+            "mbit_s": c["frames"] * g.N / dt / 1e6 if dt > 0 else None,
+            "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
+            "precision": a.precision, "schedule": a.schedule, "variant": a.variant,
+            "kernel": ctx.kernel_info(cfg)["kernel"], "rounds": res.rounds, "frames_decoded": res.frames_decoded}
+
+    _run_points(a, ck, rank, g.N, run_point)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
     return 0
 
 
-def _ems_sweep(a, seed, world, rank, device) -> int:
+def _ems_sweep(a, seed, world, rank, device, ck=None) -> int:
     """One SNR point after the other on the GF(q) EMS decoder, frames sharded as above."""
     g = native.NbGraph.from_alist(a.alist)
     ctx = native.NbContext(g, device, a.batch)
     cfg = native.EmsConfig(T=a.iterations, nm=a.nm, offset=a.offset, early_stop=not a.no_early_stop)
     bits = g.N * g.m
-    for k, snr in enumerate(a.snr):
-        def run_batch(first, n, snr=snr, k=k):
+    def run_point(k, snr, resume, on_round):
+        def run_batch(first, n):
             fr, _ = ctx.sim_batch(snr, a.rate, cfg, seed, k, first, n)
             return fr
         t0 = time.perf_counter()
         res = sim.simulate_point(run_batch, bits, a.iterations, snr, a.batch, a.min_bit_errors,
                                  a.min_frame_errors if a.min_frame_errors is not None else 40, a.max_frames,
-                                 device=device, iters_in_frames=True, first_round=a.first_round)
+                                 device=device, iters_in_frames=True, first_round=a.first_round,
+                                 resume=resume, on_round=on_round)
         dt = time.perf_counter() - t0
-        if rank == 0:
-            line = res.log_line(a.alist, [float(a.nm), a.offset])
-            if a.log:
-                with open(a.log, "a") as f:
-                    f.write(line + "\n")
-            print(line, flush=True)
-            if a.json:
-                c = res.counts
-                print(json.dumps({"ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "avg_iters": res.avg_iters,
-                                  "seconds": dt, "mbit_s": c["frames"] * bits / dt / 1e6 if dt > 0 else None,
-                                  "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
-                                  "precision": "f32", "rounds": res.rounds, "frames_decoded": res.frames_decoded}),
-                      flush=True)
+        c = res.counts
+        return res, res.log_line(a.alist, [float(a.nm), a.offset]), {
+            "ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "avg_iters": res.avg_iters,
+            "seconds": dt, "mbit_s": c["frames"] * bits / dt / 1e6 if dt > 0 else None,
+            "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
+            "precision": "f32", "rounds": res.rounds, "frames_decoded": res.frames_decoded}
+
+    _run_points(a, ck, rank, bits, run_point)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

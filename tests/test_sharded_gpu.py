@@ -177,3 +177,36 @@ def test_sweep_main_two_ranks(tmp_path):
     for a, b in zip(two, one):
         assert {k: a[k] for k in keys} == {k: b[k] for k in keys}, (a, b)
     assert log1.read_text().splitlines() == lines
+
+
+@pytest.mark.gpu
+def test_sweep_checkpoint_resume(tmp_path):
+    """SURVEY §5 checkpoint/resume on the HIP path: `sweep.py --checkpoint` writes the
+    uninterrupted run's log lines; with its .partial file cut back to mid-point
+    states (a sweep killed during point 1), a restart resumes both points and appends
+    the same lines; a restart of a finished sweep decodes and appends nothing."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = [code_path(CODE), "--rate", "0.5", "--snr", "1.5", "1.75", "-T", "50", "--variant", "nms",
+            "--alpha", "1.25", "--batch", "2048", "--seed", "777", "--json"]
+
+    def run(*extra):
+        p = subprocess.run([sys.executable, "-m", "ldpcsimulation_amd.sweep"] + args + list(extra), cwd=root,
+                           capture_output=True, text=True, timeout=600)
+        assert p.returncode == 0, p.stderr[-3000:]
+        return [json.loads(l[l.index("{"):]) for l in p.stdout.splitlines() if '"ebn0_db"' in l]
+
+    run("--log", str(tmp_path / "full.txt"))
+    want = (tmp_path / "full.txt").read_text().splitlines()
+    ck = tmp_path / "ck.partial"
+    run("--log", str(tmp_path / "a.txt"), "--checkpoint", str(ck))
+    assert (tmp_path / "a.txt").read_text().splitlines() == want
+    recs = [json.loads(l) for l in ck.read_text().splitlines()]
+    r1 = [r for r in recs if r["kind"] == "round" and r["k"] == 1]
+    assert len(r1) >= 4, len(r1)
+    kept = [r for r in recs if r["kind"] == "header" or (r["kind"] == "round" and r["k"] == 0)] + r1[:3]
+    ck.write_text("".join(json.dumps(r) + "\n" for r in kept))
+    js = run("--log", str(tmp_path / "b.txt"), "--checkpoint", str(ck))
+    assert (tmp_path / "b.txt").read_text().splitlines() == want
+    assert js[1]["resumed_from_frame"] == r1[2]["next_frame"] > 0
+    assert run("--log", str(tmp_path / "c.txt"), "--checkpoint", str(ck)) == []
+    assert not (tmp_path / "c.txt").exists()

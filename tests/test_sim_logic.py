@@ -249,3 +249,70 @@ def test_pipelined_rounds_respect_max_frames():
     res = sim.simulate_point(fake_frames, N, T, 1.5, 50, min_bit_err=10 ** 9, min_frame_err=10 ** 9,
                              max_frames=777, launcher=L)
     assert res.counts == want and not L.pending
+
+
+def _states(gen=fake_frames, batch=100, launcher=None):
+    st = []
+    res = sim.simulate_point(gen, N, T, 1.5, batch, on_round=st.append, launcher=launcher)
+    return res, st
+
+
+@pytest.mark.parametrize("batch", [7, 100, 1000])
+def test_resume_from_any_round_equals_uninterrupted(batch):
+    """SURVEY §5 checkpoint/resume: the state after any fully counted round, fed back as
+    `resume` (also with other round sizes and a launcher), gives the uninterrupted
+    run's totals and histogram: the reference's frame-by-frame result."""
+    want, hist = sequential()
+    full, states = _states(batch=batch)
+    assert full.counts == want and np.array_equal(full.hist, hist)
+    assert len(states) == full.rounds - 1            # every round but the one the stop cuts
+    for st in states:
+        assert st.acc[3] == st.next_frame           # one rank: every frame before next_frame counted
+        for b2, L in ((batch, None), (3 * batch + 1, None), (batch, _FakeLauncher())):
+            res = sim.simulate_point(fake_frames, N, T, 1.5, b2, resume=st, launcher=L)
+            assert res.counts == want and np.array_equal(res.hist, hist), (st.next_frame, b2)
+            assert res.rounds >= st.rounds
+
+
+def test_resume_state_histogram_matches_counters():
+    _, states = _states(batch=64)
+    for st in states:
+        w = np.arange(1, N + 1)
+        assert int((st.hist * w).sum()) == int(st.acc[0]) and int(st.hist.sum()) == int(st.acc[1])
+
+
+def _resume_worker(rank, world, port, q, resume):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        st = []
+        res = sim.simulate_point(fake_frames, N, T, 1.5, 50, resume=resume, on_round=st.append)
+        q.put((rank, res.counts, res.hist.tolist(), [(s.next_frame, s.acc.tolist(), s.hist.tolist()) for s in st]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_resume_two_ranks_gloo():
+    """A one-rank checkpoint resumed on two ranks (and the two ranks' own per-round
+    states, identical on both, all-reduced histogram) reproduce the sequential run."""
+    import torch.multiprocessing as mp
+    want, hist = sequential()
+    _, states = _states(batch=100)
+    mid = states[len(states) // 2]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_resume_worker, args=(r, 2, port, q, mid)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, counts, h, st in out:
+        assert counts == want and np.array_equal(np.array(h), hist), rank
+    assert out[0][3] == out[1][3]
+    for nf, acc, h in out[0][3]:
+        res = sim.simulate_point(fake_frames, N, T, 1.5, 77, resume=sim.PointState(nf, np.array(acc), np.array(h)))
+        assert res.counts == want and np.array_equal(res.hist, hist)
