@@ -16,6 +16,7 @@ the global layered kernel) is run the same way, two ranks against one, at one
 SNR point of the sweep."""
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -155,12 +156,10 @@ def test_sweep_main_two_ranks(tmp_path):
                                                                     "--log-file", str(log2)],
                        cwd=root, env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
-    seeds = {}
-    for line in p.stderr.splitlines():
-        i = line.find('{"rank"')
-        if i >= 0:
-            d = json.loads(line[i:])
-            seeds[d["rank"]] = d["seed"]
+    seeds = {}   # the two ranks' stderr lines may interleave without a newline between them
+    for m in re.finditer(r'\{"rank": \d+, "seed": \d+\}', p.stderr):
+        d = json.loads(m.group(0))
+        seeds[d["rank"]] = d["seed"]
     assert set(seeds) == {0, 1} and seeds[0] == seeds[1], seeds
     lines = log2.read_text().splitlines()
     assert len(lines) == 2, lines                       # rank 0 only, one line per point
