@@ -33,8 +33,13 @@ divided by the average launch time (HIP events on the launch stream), in
 G LDS-cycles/s; `peak` = CUs x 2.4 GHz. The SURVEY §8(d) flooding HBM
 message model (16E+4N bytes per codeword-iteration) is kept as `hbm_model`;
 it does not bound this kernel (messages never leave LDS), so its "fraction"
-exceeds 1. `traffic` = HBM bytes per launch measured by rocprofv3 PMC in
-this round (profiles/, scripts/pmc.sh).
+exceeds 1. `traffic` = HBM bytes per launch of the headline kernel, measured
+live after the timed steps: two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE;
+separate passes, MI355X_MICROARCH's counter limits) over a child run of this
+same workload (1 warm-up + 1 step), FETCH_SIZE doubled (the guide's gfx950
+correction); `traffic_gbs` = those bytes over this run's average launch time,
+against the 8 TB/s HBM peak. --live-pmc off (or running under a profiler)
+falls back to the committed PMC summary (profiles/traffic_latest.json).
 
 cpu_baseline: the reference's own decodeNMS (oracle/_ref, compiled from the
 unmodified sources) on this box's host cores, same code/variant/T/SNR.
@@ -42,8 +47,11 @@ unmodified sources) on this box's host cores, same code/variant/T/SNR.
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
 import socket
 import subprocess
 import sys
@@ -88,6 +96,8 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-procs", type=int, default=0, help="0 = the box's CPU share (see cpu_share())")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--live-pmc", choices=["auto", "off"], default="auto",
+                   help="auto: measure the headline kernel's HBM bytes with rocprofv3 --pmc child runs (N=1, rank 0)")
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend for N>1 (gloo + --share-device: rehearse N ranks on one GPU)")
     p.add_argument("--share-device", action="store_true", help="every rank on device 0 (rehearsal only)")
@@ -113,6 +123,55 @@ def host_cores() -> int:
         return len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         return os.cpu_count() or 1
+
+
+KERNEL_SYMBOL = {"rows_pp": "k_rows_pp", "rows_fast": "k_rows_fast", "rows": "k_decode_rows"}
+
+
+def pmc_kernel_average(out_dir: str, pattern: str, counter: str):
+    """Average over the dispatches of kernels matching `pattern` of one counter in a
+    rocprofv3 --output-format csv directory (per dispatch: the sum of its rows, the
+    counter's per-XCD/instance values), or None."""
+    vals = {}
+    for f in glob.glob(os.path.join(out_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if pattern in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                    vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return sum(vals.values()) / len(vals) if vals else None
+
+
+def live_traffic(args, kernel: str) -> dict:
+    """HBM bytes per launch of `kernel` in this workload, measured now: one rocprofv3
+    --pmc pass per counter (FETCH_SIZE, WRITE_SIZE) over a child bench run (1 warm-up
+    + 1 step of the headline, nothing else), each under its own time limit. Per
+    dispatch of the kernel: FETCH_SIZE x 2 (gfx950 counts wide reads at half,
+    MI355X_MICROARCH HBM section) + WRITE_SIZE, in KiB from the counters."""
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return {"error": "rocprofv3 not on PATH"}
+    pattern = KERNEL_SYMBOL.get(kernel, kernel)
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--no-secondary",
+             "--no-cpu-baseline", "--live-pmc", "off", "--precision", args.precision, "--batch", str(args.batch),
+             "--T", str(args.T), "--ebn0", str(args.ebn0), "--alpha", str(args.alpha), "--seed", str(args.seed)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    kib = {}
+    with tempfile.TemporaryDirectory(prefix="ldpc_pmc_", dir="/tmp") as d:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(d, ctr)
+            cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", ctr, "-d", out, "-o", "pmc",
+                   "--output-format", "csv", "--"] + child
+            p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True)
+            if p.returncode != 0:
+                return {"error": f"{ctr} pass rc={p.returncode}: {(p.stderr or p.stdout)[-300:]}"}
+            v = pmc_kernel_average(out, pattern, ctr)
+            if v is None:
+                return {"error": f"{ctr} pass: no {pattern} dispatch in the counter output"}
+            kib[ctr] = v
+    fetch, write = 2 * kib["FETCH_SIZE"] * 1024, kib["WRITE_SIZE"] * 1024
+    return {"hbm_bytes_per_launch": fetch + write, "fetch_bytes_x2": fetch, "write_bytes": write,
+            "kernel_pattern": pattern,
+            "source": "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over a 1-step child run of this workload"}
 
 
 def _final(out: str):
@@ -353,15 +412,21 @@ def main():
     if rank == 0:
         tot = head["tot"]
         rl = roofline(head)
-        traffic, traffic_src, traffic_kernel = None, None, None
-        try:
-            tj = json.load(open(args.traffic_json))
-            tj = tj.get(args.precision, {})
-            traffic, traffic_src, traffic_kernel = tj.get("hbm_bytes_per_launch"), tj.get("source"), tj.get("kernel")
-        except (OSError, ValueError):
-            pass
-        # the PMC bytes (a separate rocprofv3 --pmc pass of this same command, scripts/profile_round.sh)
-        # over this run's live average launch time, against the HBM peak
+        traffic, traffic_src, traffic_kernel, live = None, None, None, None
+        nested = any(k.startswith("ROCPROF") for k in os.environ) or "rocprofiler" in os.environ.get("LD_PRELOAD", "")
+        if args.live_pmc == "auto" and world == 1 and not nested:
+            live = live_traffic(args, rl["kernel"])
+            if "hbm_bytes_per_launch" in live:
+                traffic, traffic_src, traffic_kernel = live["hbm_bytes_per_launch"], live["source"], live["kernel_pattern"]
+        if traffic is None:   # the committed PMC summary of this round (scripts/profile_round.sh)
+            try:
+                tj = json.load(open(args.traffic_json))
+                tj = tj.get(args.precision, {})
+                traffic, traffic_kernel = tj.get("hbm_bytes_per_launch"), tj.get("kernel")
+                traffic_src = f"committed: {tj.get('source')}" + (f" (live pass: {live['error']})" if live else "")
+            except (OSError, ValueError):
+                pass
+        # the PMC bytes over this run's average launch time, against the HBM peak
         traffic_gbs = traffic / (rl["avg_kernel_ms"] / 1e3) / 1e9 if traffic else None
         k_fe, n_fe = int(tot[1]), int(tot[3])
         from ldpcsimulation_amd.sim import two_proportion_z, wilson_interval
@@ -389,6 +454,7 @@ def main():
                          "traffic_gbs": traffic_gbs,
                          "traffic_frac_of_hbm_peak": traffic_gbs / (HBM_PEAK / 1e9) if traffic_gbs else None,
                          "traffic_source": traffic_src, "traffic_kernel": traffic_kernel,
+                         "traffic_detail": {k: v for k, v in (live or {}).items() if k in ("fetch_bytes_x2", "write_bytes")},
                          **{k: v for k, v in rl.items() if k not in ("bound", "achieved", "peak", "unit", "frac")}},
             "fer": fer,
             "kernel_info": ctx.kernel_info(head["cfg"]),

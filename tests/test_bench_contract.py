@@ -110,3 +110,23 @@ def test_reference_fer_fixture():
         k1, n1 = b.REF_FER[p["ebn0_db"]]
         assert abs(two_proportion_z(p["frame_err"], p["frames"], k1, n1)) < 3
     assert b.reference_fer()[1.5] == (400, 27816)
+
+
+def test_pmc_kernel_average_parses_rocprof_csv(tmp_path):
+    """bench.py's live HBM traffic: per-dispatch sums of one counter over the matching
+    kernel's dispatches, averaged (other kernels and counters ignored)."""
+    import bench
+    d = tmp_path / "FETCH_SIZE" / "host" / "123"
+    d.mkdir(parents=True)
+    rows = [("1", "void ldpc::k_rows_pp<1, 8, 4, 1, true, 0>(...)", "FETCH_SIZE", "100"),
+            ("1", "void ldpc::k_rows_pp<1, 8, 4, 1, true, 0>(...)", "FETCH_SIZE", "20"),
+            ("2", "void ldpc::k_redo<...>(...)", "FETCH_SIZE", "999"),
+            ("3", "void ldpc::k_rows_pp<1, 8, 4, 1, true, 0>(...)", "FETCH_SIZE", "140"),
+            ("3", "void ldpc::k_rows_pp<1, 8, 4, 1, true, 0>(...)", "WRITE_SIZE", "5")]
+    with open(d / "pmc_counter_collection.csv", "w") as f:
+        f.write("Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value\n")
+        for r in rows:
+            f.write(",".join(f'"{x}"' for x in r) + "\n")
+    assert bench.pmc_kernel_average(str(tmp_path / "FETCH_SIZE"), "k_rows_pp", "FETCH_SIZE") == 130.0
+    assert bench.pmc_kernel_average(str(tmp_path / "FETCH_SIZE"), "k_rows_fast", "FETCH_SIZE") is None
+    assert bench.KERNEL_SYMBOL["rows_pp"] == "k_rows_pp"
