@@ -152,16 +152,20 @@ __device__ __forceinline__ PPSlots pp_slots(unsigned char *smem, int N, int EA)
     return s;
 }
 
-// Channel of the pair (:214-238) staged into app[X][v] (v < N), by all 1024
-// threads, 4 bits (one Philox call) per thread and step; unc[X] = this thread's
-// uncoded errors of slot X.
+// Channel of the pair (:214-238) staged into app[X][v] (v < N), by the bit role
+// (threads t0, t0 + nt, ...), 4 bits (one Philox call) per thread and step;
+// unc[X] = this thread's uncoded errors of slot X. The check role stays out of
+// it: with the f64 Box-Muller inlined into its pair loop, the compiler hoisted
+// the channel's loop invariants and spilled 14 doubles per thread around every
+// pair's interval loop (1.2 GB of scratch write-backs per bench launch).
 template <int SRC>
-__device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots &s, int N, int grp, int (&unc)[2])
+__device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots &s, int N, int grp, int (&unc)[2],
+                                           int t0, int nt)
 {
     using F = double;
     unc[0] = unc[1] = 0;
     const int ng4 = (N + 3) / 4;
-    for (int t = threadIdx.x; t < 2 * ng4; t += blockDim.x) {
+    for (int t = t0; t < 2 * ng4; t += nt) {
         const int X = t >= ng4 ? 1 : 0, g4 = t - X * ng4;
         const int b = grp * 2 + X;
         if (b >= a.batch) continue;
@@ -296,8 +300,8 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
     const int npairs = (a.batch + 1) / 2;
     PP_STAMP_DECL;
     for (int grp = blockIdx.x; grp < npairs; grp += gridDim.x) {
-        int unc[2];
-        pp_channel<SRC>(a, s, N, grp, unc);
+        int unc[2] = {0, 0};
+        if constexpr (HB) pp_channel<SRC>(a, s, N, grp, unc, bt, kPPRole);
         __syncthreads();   // B1: channel staged
         [[maybe_unused]] P yq[2][CPT];
         if constexpr (R > 0) {
