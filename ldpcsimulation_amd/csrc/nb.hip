@@ -241,7 +241,9 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
 #pragma unroll
         for (int a = 0; a < Q; ++a) {
             const int p = ((a & 1) ? h1 : 0) ^ ((a & 2) ? h2 : 0) ^ ((a & 4) ? h4 : 0) ^ ((a & 8) ? h8 : 0) ^ f;
-            ad[a] = (((p >> 2) * Ep + s) << 2) + (p & 3);
+            // (p >> 2) < 4 and Ep < 2^24: one full-rate v_mad_u32_u24 (the plain product
+            // compiled to quarter-rate v_mul_lo_u32 / v_mad_u64_u32, 64 per symbol-node pass)
+            ad[a] = (int)((__umul24((unsigned)(p >> 2), (unsigned)Ep) + (unsigned)s) << 2) + (p & 3);
         }
     };
     int ad[Q];
