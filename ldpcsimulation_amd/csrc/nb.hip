@@ -52,10 +52,8 @@ constexpr float kInf = __builtin_huge_valf();
 // with Ep = slots rounded to 2 mod 8 (spreads the symbol-node gathers over
 // the banks).
 struct NbSched {
-    int Ep;
+    int Ep, M;
     const uint8_t *cn_d;     // [M]    check degree
-    const uint16_t *ecol;    // [Ms]   symbol of each slot (syndrome)
-    const uint8_t *eh;       // [Ms]   coefficient of each slot
     const uint32_t *vn;      // [N]    first col entry << 8 | degree
     const uint16_t *vslot;   // [E]    slots of each symbol, nlist order
     const uint8_t *vh;       // [E]    their coefficients
@@ -63,29 +61,6 @@ struct NbSched {
 
 // GF(16) (x^4 + x + 1): v * x.
 __device__ __forceinline__ int gf16_xt(int v) { return ((v << 1) & 15) ^ ((v & 8) ? 3 : 0); }
-
-template <int Q>
-__device__ __forceinline__ int syndrome_fail(const NbDevGraph &g, const NbSched &s, const uint8_t *dec,
-                                             const uint8_t *gmul)
-{
-    int fail = 0;
-    for (int j = threadIdx.x; j < g.M; j += blockDim.x) {
-        const int d = s.cn_d[j];
-        int sy = 0;
-        for (int k = 0; k < d; ++k) {
-            const int sl = k * g.M + j;
-            if (Q == 16) {   // h * dec by xtime in registers (one LDS round trip less than the table)
-                const int h1 = s.eh[sl], x = dec[s.ecol[sl]];
-                const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
-                sy ^= ((x & 1) ? h1 : 0) ^ ((x & 2) ? h2 : 0) ^ ((x & 4) ? h4 : 0) ^ ((x & 8) ? h8 : 0);
-            } else {
-                sy ^= gmul[s.eh[sl] * Q + dec[s.ecol[sl]]];
-            }
-        }
-        fail |= sy != 0;
-    }
-    return __syncthreads_or(fail);
-}
 
 // ---- check node: one lane per (check, direction), the message vectors in registers ----
 template <int Q>
@@ -210,9 +185,37 @@ __device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int di
 // Entry a (symbol domain) of an edge's message lives at check-domain position
 // h*a. init: write v2c = L on every edge. Otherwise app = L + sum of the c2v
 // (nlist order), decision argmin app (first minimum), v2c = (app - c2v) - min.
-template <int Q, int MB, int VD>
+// This symbol's share of the parity checks of the new decisions: h * dec xor-ed
+// into its checks' syndrome bytes (slot = k*M + j: check j = slot mod M, k < DC).
+// GF(16) sums are xors, so the order of the atomics does not matter.
+template <int DC>
+__device__ __forceinline__ void vn_syndrome(const NbSched &sc, int e0, int e1, int d, uint32_t *synd)
+{
+    for (int e = e0; e < e1; ++e) {
+        int j = sc.vslot[e];
+#pragma unroll
+        for (int k = 1; k < DC; ++k) j -= j >= sc.M ? sc.M : 0;
+        const int h1 = sc.vh[e] & 15, h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
+        const int hd = ((d & 1) ? h1 : 0) ^ ((d & 2) ? h2 : 0) ^ ((d & 4) ? h4 : 0) ^ ((d & 8) ? h8 : 0);
+        if (hd) atomicXor(&synd[j >> 2], (uint32_t)hd << (8 * (j & 3)));
+    }
+}
+
+// After the symbol phase's barrier: any check unsatisfied? Every syndrome word is
+// read and cleared (the next contributions come after the next check phase's barrier).
+__device__ __forceinline__ int syndrome_read_reset(uint32_t *synd, int nw)
+{
+    int fail = 0;
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+        fail |= synd[w] != 0u;
+        synd[w] = 0u;
+    }
+    return __syncthreads_or(fail);
+}
+
+template <int Q, int MB, int VD, int DC>
 __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched &sc, const float *lam, uint8_t *dec,
-                                        bool init)
+                                        bool init, uint32_t *synd)
 {
     static_assert(Q == 16 && MB == 4, "GF(16)");
     const float4 l4 = *reinterpret_cast<const float4 *>(lam + v * MB);
@@ -282,6 +285,7 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
                 best = a;
             }
         dec[v] = (uint8_t)best;
+        vn_syndrome<DC>(sc, e0, e1, best, synd);
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (k < deg) {
@@ -311,6 +315,7 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
             best = a;
         }
     dec[v] = (uint8_t)best;
+    vn_syndrome<DC>(sc, e0, e1, best, synd);
     if (init) return;
     for (int e = e0; e < e1; ++e) {
         addr(e, ad);
@@ -327,7 +332,7 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
 
 template <int Q, int MB, int DC, int SRC>
 __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &g, int b, float *msg, float *lam,
-                                             uint8_t *dec, const uint8_t *gmul, const NbSched &sc, int *red)
+                                             uint8_t *dec, const NbSched &sc, int *red, uint32_t *synd)
 {
     const int tid = threadIdx.x, nt = blockDim.x;
     const int N = g.N, M = g.M, Ep = sc.Ep;
@@ -368,9 +373,9 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     }
     __syncthreads();
     // ---- initial messages v2c = L (stored at the check-domain position h*x), decisions argmin L ----
-    for (int v = tid; v < N; v += nt) vn_lane<Q, MB, 0>(msg, Ep, v, sc, lam, dec, true);
+    for (int v = tid; v < N; v += nt) vn_lane<Q, MB, 0, DC>(msg, Ep, v, sc, lam, dec, true, synd);
     __syncthreads();
-    int fail = syndrome_fail<Q>(g, sc, dec, gmul);
+    int fail = syndrome_read_reset(synd, (M + 3) / 4);
     int it = 0;
     // check lanes: in each wave, lanes 0-31 take 32 consecutive checks in mlist
     // order and lanes 32-63 the same checks reversed
@@ -404,9 +409,9 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         __syncthreads();
         // ---- symbol nodes: lane x = variable-domain symbol, reads c2v(x) at position h*x ----
         for (int v = tid; v < N && LDPC_EMS_EXP != 2; v += nt)
-            vn_lane<Q, MB, LDPC_EMS_VD>(msg, Ep, v, sc, lam, dec, false);
+            vn_lane<Q, MB, LDPC_EMS_VD, DC>(msg, Ep, v, sc, lam, dec, false, synd);
         __syncthreads();
-        if (LDPC_EMS_EXP != 3) fail = syndrome_fail<Q>(g, sc, dec, gmul);
+        if (LDPC_EMS_EXP != 3) fail = syndrome_read_reset(synd, (M + 3) / 4);
         ++it;
     }
 
@@ -436,13 +441,13 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 
-// dynamic LDS: [msg 16*Ep f32 (ems_lds only)] [lam N*m f32] [dec N u8] [gf_mul Q*Q u8] [cn_d M u8]
-//              [ecol Ms u16] [eh Ms u8] [vn N u32] [vslot E u16] [vh E u8]
+// dynamic LDS: [msg 16*Ep f32 (ems_lds only)] [lam N*m f32] [dec N u8] [cn_d M u8]
+//              [vn N u32] [vslot E u16] [vh E u8] [synd ceil(M/4) u32]
 __host__ __device__ inline size_t aux_bytes(const NbDevGraph &g)
 {
-    const size_t ms = (size_t)g.maxdc * g.M;
-    return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.q * g.q) + align16((size_t)g.M) +
-           align16(ms * 2) + align16(ms) + align16((size_t)g.N * 4) + align16((size_t)g.E * 2) + align16((size_t)g.E);
+    return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.M) +
+           align16((size_t)g.N * 4) + align16((size_t)g.E * 2) + align16((size_t)g.E) +
+           align16((size_t)(g.M + 3) / 4 * 4);
 }
 
 template <int Q, int MB, int DC, int SRC, bool GSTATE, int THREADS>
@@ -452,7 +457,6 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     __shared__ int red[16 * 3];
     const int Ep = nb_ep(g);
-    const size_t ms = (size_t)g.maxdc * g.M;
     unsigned char *p = smem;
     float *msg;
     if (GSTATE) {
@@ -465,28 +469,17 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
     p += align16((size_t)g.N * MB * 4);
     uint8_t *dec = p;
     p += align16((size_t)g.N);
-    uint8_t *gmul = p;
-    p += align16((size_t)Q * Q);
     uint8_t *cn_d = p;
     p += align16((size_t)g.M);
-    uint16_t *ecol = reinterpret_cast<uint16_t *>(p);
-    p += align16(ms * 2);
-    uint8_t *eh = p;
-    p += align16(ms);
     uint32_t *vn = reinterpret_cast<uint32_t *>(p);
     p += align16((size_t)g.N * 4);
     uint16_t *vslot = reinterpret_cast<uint16_t *>(p);
     p += align16((size_t)g.E * 2);
     uint8_t *vh = p;
-    for (int i = threadIdx.x; i < Q * Q; i += blockDim.x) gmul[i] = g.gf_mul[i];
-    for (int j = threadIdx.x; j < g.M; j += blockDim.x) {
-        const int r0 = g.row_ptr[j], d = g.row_ptr[j + 1] - r0;
-        cn_d[j] = (uint8_t)d;
-        for (int k = 0; k < d; ++k) {
-            ecol[k * g.M + j] = (uint16_t)g.row_col[r0 + k];
-            eh[k * g.M + j] = g.row_h[r0 + k];
-        }
-    }
+    p += align16((size_t)g.E);
+    uint32_t *synd = reinterpret_cast<uint32_t *>(p);   // check j: byte j & 3 of word j >> 2
+    for (int w = threadIdx.x; w < (g.M + 3) / 4; w += blockDim.x) synd[w] = 0u;
+    for (int j = threadIdx.x; j < g.M; j += blockDim.x) cn_d[j] = (uint8_t)(g.row_ptr[j + 1] - g.row_ptr[j]);
     for (int v = threadIdx.x; v < g.N; v += blockDim.x)
         vn[v] = ((uint32_t)g.col_ptr[v] << 8) | (uint32_t)(g.col_ptr[v + 1] - g.col_ptr[v]);
     for (int e = threadIdx.x; e < g.E; e += blockDim.x) {
@@ -494,9 +487,9 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
         vh[e] = g.col_h[e];
     }
     __syncthreads();
-    const NbSched sc{Ep, cn_d, ecol, eh, vn, vslot, vh};
+    const NbSched sc{Ep, g.M, cn_d, vn, vslot, vh};
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
-        ems_codeword<Q, MB, DC, SRC>(a, g, b, msg, lam, dec, gmul, sc, red);
+        ems_codeword<Q, MB, DC, SRC>(a, g, b, msg, lam, dec, sc, red, synd);
 }
 
 constexpr size_t kNbMaxLds = 160 * 1024;

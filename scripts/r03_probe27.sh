@@ -1,6 +1,6 @@
 #!/bin/bash
-# EMS symbol-node addresses by 24-bit multiplies: parity (test_ems.py), A/B against
-# the previous build at 1.5 / 2.0 dB.
+# EMS: parity (test_ems.py), then A/B against the previous build (LDPC_LIB=emsold)
+# at 1.5 / 2.0 dB.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/${RUN_TAG:-r03p27}; mkdir -p $O
