@@ -1,8 +1,7 @@
 #!/bin/bash
-# Round-3 close evidence at HEAD (second session): full GPU suite + smoke, the
-# default bench line (live PMC traffic, CPU baseline), kernel stats + HBM/SQ PMC of
-# the headline, the EMS profile and SNR rates. Each step under its own limit; the
-# first failure ends the run.
+# Round-3 close evidence at HEAD (second session), part A: full GPU suite + smoke
+# and the default bench line (live PMC traffic, CPU baseline); part B is
+# r03b_close_b.sh. Each step under its own limit; the first failure ends the run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -12,7 +11,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 echo "smoke: $(tail -1 $O/smoke.log | cut -c1-200)"
 timeout -k 10 600 python bench.py > $O/bench.jsonl 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
 python -c "import json; d=json.loads(open('$O/bench.jsonl').read().splitlines()[-1]); r=d['roofline']; print('bench', round(d['value']), round(d['ms_per_step'],3), 'frac', round(r['frac'],4), 'traffic', r['traffic'], 'GB/s', r['traffic_gbs'], 'cpu', d.get('cpu_baseline',{}).get('value'), 'f32', d['f32']['value'])"
-RUN_TAG=r03b_close_prof BENCH_ARGS="--no-secondary" bash scripts/profile_round.sh || exit 1
-RUN_TAG=r03b_close_ems bash scripts/profile_ems.sh || exit 1
-timeout -k 10 300 python3 scripts/bench_ems.py --ebn0 1.0 1.5 2.0 2.5 --steps 3 > $O/bench_ems.jsonl 2>&1 || { tail -5 $O/bench_ems.jsonl; exit 1; }
 echo done
