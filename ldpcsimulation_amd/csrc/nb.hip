@@ -182,9 +182,6 @@ __device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int di
 // the powers in a.
 
 // ---- symbol node: one lane per symbol, the 16-entry vectors in registers ----
-// Entry a (symbol domain) of an edge's message lives at check-domain position
-// h*a. init: write v2c = L on every edge. Otherwise app = L + sum of the c2v
-// (nlist order), decision argmin app (first minimum), v2c = (app - c2v) - min.
 // This symbol's share of the parity checks of the new decisions: h * dec xor-ed
 // into its checks' syndrome bytes (slot = k*M + j: check j = slot mod M, k < DC).
 // GF(16) sums are xors, so the order of the atomics does not matter.
@@ -213,6 +210,10 @@ __device__ __forceinline__ int syndrome_read_reset(uint32_t *synd, int nw)
     return __syncthreads_or(fail);
 }
 
+// Entry a (symbol domain) of an edge's message lives at check-domain position
+// h*a. init: write v2c = L on every edge. Otherwise app = L + sum of the c2v
+// (nlist order), decision argmin app (first minimum), v2c = (app - c2v) - min.
+// Both add the new decision's syndrome contributions (vn_syndrome).
 template <int Q, int MB, int VD, int DC>
 __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched &sc, const float *lam, uint8_t *dec,
                                         bool init, uint32_t *synd)

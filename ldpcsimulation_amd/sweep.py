@@ -118,7 +118,6 @@ def _run_points(a, ck, rank, n_hist, run_point):
             ck.save_done(k, snr, line)
 
 
-
 def main(argv=None) -> int:
     a = parse(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,9 +190,10 @@ def main(argv=None) -> int:
                                  resume=resume, on_round=on_round)
         dt = time.perf_counter() - t0
         c = res.counts
+        ran = c["frames"] - (int(resume.acc[3]) if resume else 0)   # frames counted by this run
         return res, res.log_line(a.alist, extra), {
             "ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "seconds": dt,
-            "mbit_s": c["frames"] * g.N / dt / 1e6 if dt > 0 else None,
+            "mbit_s": ran * g.N / dt / 1e6 if dt > 0 else None,
             "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
             "precision": a.precision, "schedule": a.schedule, "variant": a.variant,
             "kernel": ctx.kernel_info(cfg)["kernel"], "rounds": res.rounds, "frames_decoded": res.frames_decoded}
@@ -222,9 +222,10 @@ def _ems_sweep(a, seed, world, rank, device, ck=None) -> int:
                                  resume=resume, on_round=on_round)
         dt = time.perf_counter() - t0
         c = res.counts
+        ran = c["frames"] - (int(resume.acc[3]) if resume else 0)   # frames counted by this run
         return res, res.log_line(a.alist, [float(a.nm), a.offset]), {
             "ebn0_db": snr, **c, "ber": res.ber, "fer": res.fer, "avg_iters": res.avg_iters,
-            "seconds": dt, "mbit_s": c["frames"] * bits / dt / 1e6 if dt > 0 else None,
+            "seconds": dt, "mbit_s": ran * bits / dt / 1e6 if dt > 0 else None,
             "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
             "precision": "f32", "rounds": res.rounds, "frames_decoded": res.frames_decoded}
 
