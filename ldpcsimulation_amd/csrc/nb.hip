@@ -11,12 +11,14 @@
 //     lanes of a check (same wave, lockstep) split the forward-backward
 //     (cn_lane); messages are read and written as 4 x 16-byte chunks;
 //   symbol node: one lane per symbol, entry a of an edge gathered from its
-//     check-domain position h*a (GF(16) products by xtime in registers).
-// One 512-thread workgroup decodes one codeword at a time (persistent over
-// the batch); its edge messages (16 fp32 per edge, in place: c2v after the
-// check phase, v2c after the symbol phase) and bit LLRs live in LDS when they
-// fit (128 KB of messages for N = 1000, E = 2000), else in a global slot per
-// workgroup.
+//     check-domain position h*a (GF(16) products by xtime in registers); it
+//     also xors h*dec into its checks' syndrome bytes (LDS atomics), read and
+//     cleared after the phase for the early stop.
+// One workgroup (1024 threads for row degree <= 4, 512 for <= 8) decodes one
+// codeword at a time (persistent over the batch); its edge messages (16 fp32
+// per edge, in place: c2v after the check phase, v2c after the symbol phase)
+// and bit LLRs live in LDS when they fit (128 KB of messages for N = 1000,
+// E = 2000), else in a global slot per workgroup.
 #include "nb.h"
 #include "device_common.h"
 #include "kernels.h"
