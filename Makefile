@@ -31,12 +31,17 @@ KERNFLAGS = -Xclang -target-feature -Xclang -load-store-opt
 # by up to 4 % with the code layout (s_nop shifts at the kernel entry: 14.85-15.47
 # ms); aligned, 14.78-14.85 ms for every shift.
 ALIGNFLAGS = -falign-loops=32
+# The ping-pong kernel under LLVM's max-memory-clause machine scheduler: its LDS
+# reads issue in clauses ahead of their uses; 14.29-14.48 vs 14.65-14.77 ms per
+# bench launch over 3 interleaved rounds, stable under code shifts;
+# `make ppvariant PPSCHED= VFLAGS="-mllvm -amdgpu-sched-strategy=..."` for others.
+PPSCHED ?= -mllvm -amdgpu-sched-strategy=max-memory-clause
 $(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/rows_fast.o: $(CSRC)/rows_fast.hip $(CSRC)/fast64.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/rows_pp.o: $(CSRC)/rows_pp.hip $(CSRC)/fast64.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) -c -o $@ $<
 $(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/bp.o: $(CSRC)/bp.hip $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
@@ -107,7 +112,7 @@ fastvariant: $(OBJS)
 # Ping-pong kernel A/B variants: make ppvariant NAME=x VFLAGS="-DLDPC_PP_..." -> lib/variants/libldpc_hip_x.so
 ppvariant: $(OBJS)
 	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o $(CSRC)/rows_pp.hip
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o $(CSRC)/rows_pp.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/rows_pp.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o
 
