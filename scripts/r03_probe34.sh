@@ -1,0 +1,7 @@
+#!/bin/bash
+# Knobs on top of the max-memory-clause ping-pong default (A/B, 2 rounds).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+A=("LDPC_ROWS=pp")
+for n in ppcnofence ppcprio3 ppcu48 ppcu12; do A+=("LDPC_ROWS=pp LDPC_LIB=$n"); done
+bash scripts/ab_multi.sh 2 "${A[@]}" -- --no-secondary --steps 5 --warmup 1 --live-pmc off
