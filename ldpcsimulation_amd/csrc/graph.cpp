@@ -88,9 +88,31 @@ std::string build_graph(int N, int M, const int *num_nlist, const int *const *nl
     return "";
 }
 
-std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, int rpt, RowSchedule &s)
+std::vector<int> pp_row_slots(const ldpc_graph &g, int threads, int dc_low)
+{
+    const int half = threads / 2;
+    if (threads % 128 || g.M > 2 * threads) return {};
+    // capped slots in fill order: row 0 of every thread, then row 1 of threads half..threads-1
+    std::vector<int> capped, open, out(2 * (size_t)threads, -1);
+    for (int t = 0; t < threads; ++t) capped.push_back(t);
+    for (int t = half; t < threads; ++t) capped.push_back(threads + t);
+    for (int t = 0; t < half; ++t) open.push_back(threads + t);
+    size_t nc = 0, no = 0;
+    std::vector<int> rest;
+    for (int j = 0; j < g.M; ++j) {
+        if (g.row_deg[j] <= dc_low && nc < capped.size()) out[capped[nc++]] = j;
+        else rest.push_back(j);
+    }
+    if (rest.size() > open.size()) return {};
+    for (int j : rest) out[open[no++]] = j;
+    return out;
+}
+
+std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, int rpt, RowSchedule &s,
+                               const std::vector<int> *row_of_slot)
 {
     if (threads % 64 || (long)threads * rpt < g.M) return "rows exceed threads";
+    if (row_of_slot && row_of_slot->size() != (size_t)threads * rpt) return "row slot map has the wrong size";
     if ((long)threads * cpt < g.N) return "bits exceed slots";
     if (g.maxdc > dc) return "row degree exceeds kernel bound";
     if (g.N > 65534) return "N exceeds 16-bit schedule";
@@ -143,10 +165,18 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
             s.cn_cols[(size_t)t * dc + k] = (uint16_t)g.N;
             s.cn_pos[(size_t)t * dc + k] = (uint16_t)(s.e_pad + (t & 63));
         }
+    std::vector<int> slot_of(g.M, -1);   // row -> its slot
+    for (int t = 0; t < rows; ++t) {
+        const int j = row_of_slot ? (*row_of_slot)[t] : (t < g.M ? t : -1);
+        if (j < -1 || j >= g.M || (j >= 0 && slot_of[j] >= 0)) return "row slot map is not a permutation";
+        if (j >= 0) slot_of[j] = t;
+    }
     for (int j = 0; j < g.M; ++j) {
-        s.cn_deg[j] = g.row_deg[j];
+        const int t = slot_of[j];
+        if (t < 0) return "row slot map misses a row";
+        s.cn_deg[t] = g.row_deg[j];
         for (int k = 0; k < g.row_deg[j]; ++k)
-            s.cn_cols[(size_t)j * dc + k] = (uint16_t)g.row_cols[(size_t)j * std::max(g.maxdc, 1) + k];
+            s.cn_cols[(size_t)t * dc + k] = (uint16_t)g.row_cols[(size_t)j * std::max(g.maxdc, 1) + k];
     }
     for (int grp = 0; grp < ngroups; ++grp) {
         for (int l = 0; l < 64; ++l) {
@@ -160,7 +190,7 @@ std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc
             for (int kc = 0; kc < d; ++kc) {
                 const uint32_t ref = g.col_refs[g.col_ptr[v] + kc];
                 const int j = (int)(ref >> kRefShift), kr = (int)(ref & ((1u << kRefShift) - 1));
-                s.cn_pos[(size_t)j * dc + kr] = (uint16_t)(gbase[grp] + kc * 64 + l);
+                s.cn_pos[(size_t)slot_of[j] * dc + kr] = (uint16_t)(gbase[grp] + kc * 64 + l);
             }
         }
     }

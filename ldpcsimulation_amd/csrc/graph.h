@@ -36,6 +36,7 @@ constexpr int kRefShift = 6;
 // longest-processing-time so the bit-node phase is balanced across waves.
 struct RowSchedule {
     int threads = 0, cpt = 0, dc = 0, e_pad = 0, rpt = 1;
+    int dc_low = 0;                  // > 0: rows placed by pp_row_slots (slots it caps hold degree <= dc_low)
     std::vector<uint16_t> cn_cols;   // [threads * rpt * dc]  bit index of edge k of row j
     std::vector<uint16_t> cn_pos;    // [threads * rpt * dc]  c2v element of edge k of row j
     std::vector<uint8_t> cn_deg;     // [threads * rpt]       (row j -> thread j % threads)
@@ -102,5 +103,18 @@ std::string load_alist(const char *path, ldpc_graph &g);
 // Row schedule for `threads` threads (multiple of 64, >= M), `cpt` bit slots
 // per thread (threads*cpt >= N) and row-degree bound dc. Returns "" or why the
 // graph does not fit (the caller then uses the generic kernel).
-std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, int rpt, RowSchedule &s);
+// row_of_slot (optional, [threads * rpt], -1 = padding): the check row each row
+// slot holds; by default slot j holds row j. Any assignment gives the same
+// values (flooding rows are independent); it only moves work between waves.
+std::string build_row_schedule(const ldpc_graph &g, int threads, int cpt, int dc, int rpt, RowSchedule &s,
+                               const std::vector<int> *row_of_slot = nullptr);
+// Degree-aware row slots of the ping-pong kernel (rows_pp.hip; 512 check threads,
+// 2 rows each, dc 8): every row-0 slot and the row-1 slots of threads 256..511
+// -- the younger check wave of each SIMD runs only those -- hold rows of degree
+// <= dc_low (a 7-edge check node: 7 gathers, 7 scatters, a 7-input tournament);
+// the degree-8 rows, the remaining rows and the padding go to the row-1 slots
+// of threads 0..255. Rows keep their order within each class (quasi-cyclic
+// neighbours stay lane neighbours: coalesced gathers and scatters). Empty when
+// the rows do not fit that split.
+std::vector<int> pp_row_slots(const ldpc_graph &g, int threads, int dc_low);
 }  // namespace ldpc

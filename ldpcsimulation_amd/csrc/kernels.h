@@ -43,7 +43,8 @@ struct DecodeArgs {
 // Device copy of graph.h's RowSchedule (row-parallel kernel).
 struct RowSched {
     int threads, cpt, dc, e_pad, rpt;
-    const uint16_t *cn_cols;        // [threads * rpt * dc]  (row j = thread j % threads, r = j / threads)
+    int dc_low;                     // > 0: degree-aware row slots (graph.h pp_row_slots)
+    const uint16_t *cn_cols;       // [threads * rpt * dc]  (row j = thread j % threads, r = j / threads)
     const uint16_t *cn_pos;         // [threads * rpt * dc]
     const uint8_t *cn_deg;          // [threads * rpt]
     const uint16_t *vn_col;         // [threads * cpt]

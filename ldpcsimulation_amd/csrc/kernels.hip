@@ -846,20 +846,24 @@ __global__ __launch_bounds__(256) void k_flood_account(DecodeArgs a, int b0, int
 }
 
 // Messages between the phases: the packed row state (default) or the c2v
-// array (LDPC_FLOOD_MSG=c2v).
-static bool flood_packed()
+// array (LDPC_FLOOD_MSG=c2v). The packed bit phase is built for column degrees
+// up to 32 (k_flood_bit_packed<F, 8|16|32>); a code with a heavier column takes
+// the c2v array, whose bit phase has an any-degree instance (DV = 0).
+constexpr int kFloodPackedMaxDv = 32;
+static bool flood_packed(const FloodSched &fs)
 {
+    if (fs.dv > kFloodPackedMaxDv) return false;
     const char *e = std::getenv("LDPC_FLOOD_MSG");
     return !(e && std::strcmp(e, "c2v") == 0);
 }
 
 // Resident slots per step of the check (LDPC_FLOOD_SPS_CHECK) and bit
 // (LDPC_FLOOD_SPS_BIT) phase kernels.
-static int flood_sps(bool check)
+static int flood_sps(bool check, const FloodSched &fs)
 {
     const char *e = std::getenv(check ? "LDPC_FLOOD_SPS_CHECK" : "LDPC_FLOOD_SPS_BIT");
     if (e) return std::max(1, std::atoi(e));
-    return check || flood_packed() ? 1 : 2;   // packed bit phase: 1 (2 204 vs 2 124 Mbit/s fp32)
+    return check || flood_packed(fs) ? 1 : 2;   // packed bit phase: 1 (2 204 vs 2 124 Mbit/s fp32)
 }
 
 // Resident codewords of the phase-per-launch flooding: the state the phases
@@ -914,8 +918,8 @@ struct FloodHalf {
         const dim3 cg((NPc + 255) / 256, (n + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW);
 #endif
         unsigned char *sc = scratch + sb * (size_t)lo;
-        const int sps = flood_sps(true);
-        const bool packed = flood_packed();
+        const int sps = flood_sps(true, *fs);
+        const bool packed = flood_packed(*fs);
 #define CHK(DC, SPS)                                                                                     \
     do {                                                                                                 \
         if (packed) hipLaunchKernelGGL((k_flood_check<F, DC, SPS, false>), cg, dim3(256), 0, s, *a, *fs, sc, sb, n); \
@@ -943,8 +947,8 @@ struct FloodHalf {
         const dim3 bg((NP + 255) / 256, (n + LDPC_FLOOD_CPW - 1) / LDPC_FLOOD_CPW);
 #endif
         unsigned char *sc = scratch + sb * (size_t)lo;
-        const int sps = flood_sps(false);
-        if (flood_packed()) {
+        const int sps = flood_sps(false, *fs);
+        if (flood_packed(*fs)) {
             if (fs->dv <= 8) {
                 if (sps >= 2) hipLaunchKernelGGL((k_flood_bit_packed<F, 8, 2>), bg, dim3(256), 0, s, *fs, sc, sb, n);
                 else hipLaunchKernelGGL((k_flood_bit_packed<F, 8, 1>), bg, dim3(256), 0, s, *fs, sc, sb, n);
@@ -996,7 +1000,7 @@ static hipError_t launch_flood_phase_t(const DevGraph &g, const FloodSched &fs, 
 {
     const size_t sb = kc.scratch_per_block;
     const size_t c2v_bytes = (size_t)((fs.e_pad + 64 + 1) / 2 * 2) * sizeof(F);
-    const int K = flood_phase_resident(sb, flood_packed() ? sb - c2v_bytes : sb, gs_bytes);
+    const int K = flood_phase_resident(sb, flood_packed(fs) ? sb - c2v_bytes : sb, gs_bytes);
     unsigned char *scratch = (unsigned char *)gs;
     int *unc = reinterpret_cast<int *>(scratch + sb * (size_t)K);   // per-slot counters after the slots
     int *wsum = unc + K, *ssum = wsum + K;

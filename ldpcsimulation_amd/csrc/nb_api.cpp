@@ -169,9 +169,14 @@ static std::vector<uint8_t> nb_swizzled_coefficients(const ldpc_nb_graph &g, con
         for (int k = 0; k < DV; ++k) C[(size_t)grp * DV + k] = gcost(grp, k);
     uint32_t x = 0x9e3779b9u;
     auto rnd = [&]() { x ^= x << 13; x ^= x >> 17; x ^= x << 5; return x; };
+    // a move needs two slots of one check: only checks of degree >= 2 take part
+    std::vector<int> rows2;
+    for (int j = 0; j < M; ++j)
+        if (g.row_ptr[j + 1] - g.row_ptr[j] >= 2) rows2.push_back(j);
+    if (rows2.empty()) return out;
     const long moves = std::min(200000L, 40L * g.E);
     for (long it = 0; it < moves; ++it) {
-        const int j = (int)(rnd() % (uint32_t)M), d = g.row_ptr[j + 1] - g.row_ptr[j];
+        const int j = rows2[rnd() % (uint32_t)rows2.size()], d = g.row_ptr[j + 1] - g.row_ptr[j];
         const int k1 = (int)(rnd() % (uint32_t)d);
         int k2 = (int)(rnd() % (uint32_t)(d - 1));
         if (k2 >= k1) ++k2;

@@ -64,7 +64,8 @@ namespace {
 #endif
 
 // Wave priority (s_setprio): 0 none, 1 check role above the bit role, 2 the reverse,
-// 3 the younger half of each role (waves 4-7, 12-15) above the older half.
+// 3 the younger half of each role (waves 4-7, 12-15) above the older half, 4 the younger
+// check waves (4-7) above all others, 5 younger check > older check > bit waves.
 #ifndef LDPC_PP_PRIO
 #define LDPC_PP_PRIO 0
 #endif
@@ -98,35 +99,22 @@ namespace {
 #endif
 
 constexpr int kPPRole = 512;          // threads per role
-constexpr int kPPRedInts = 160;       // [0,2): slot flags; [2]: sync abort; [4,8): sync counters;
-                                      // [32,128): block sums; [128,140): acc (6 x u64)
-constexpr int kPPSyncAbort = 2, kPPCheckDone = 4, kPPBitDone = 6;   // red[] indices (counters per slot)
-constexpr unsigned kPPSpinLimit = 1u << 22;   // polls (~64 cycles apart) before a wait gives up
+constexpr int kPPWaves = 2 * kPPRole / 64;
+constexpr int kPPRedSums = 32;        // red[] ints: [0,2) slot flags, [32,128) block sums, [128,140) acc (6 x u64)
+constexpr int kPPRedAcc = 128;
+constexpr int kPPRedInts = 160;
+static_assert(kPPRedSums + kPPWaves * 6 <= kPPRedAcc, "block sums overlap acc");
+static_assert(kPPRedAcc % 2 == 0 && kPPRedAcc + 2 * 6 <= kPPRedInts, "acc (6 x u64) outside red[]");
 
-// Dataflow sync (MODE 2): LDS counters instead of block barriers. A wave waits
-// (polling, s_sleep between polls) until counter c reaches `target`, then
-// acquires; the producer side releases (all its LDS writes complete) and adds 1
-// per wave. A wait that never ends (a bug) gives up after kPPSpinLimit polls,
-// raises the abort word -- every other wait of the block then gives up within
-// 256 polls, so the grid drains -- and the host reports it (counts[7],
-// ldpc_ctx_read_counts).
-__device__ __forceinline__ void pp_wait(int *red, int c, int target)
+// f(integral_constant<int, I>) for I = B .. E-1: a row loop whose index is a
+// compile-time constant (each row slot has its own compile-time degree)
+template <int B, int E, typename Fn>
+__device__ __forceinline__ void static_for(Fn &&f)
 {
-    unsigned n = 0;
-#pragma nounroll
-    while (__builtin_amdgcn_readfirstlane(__atomic_load_n(&red[c], __ATOMIC_RELAXED)) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if ((++n & 255u) == 0 && (n >= kPPSpinLimit || __atomic_load_n(&red[kPPSyncAbort], __ATOMIC_RELAXED))) {
-            __atomic_store_n(&red[kPPSyncAbort], 1, __ATOMIC_RELAXED);
-            break;
-        }
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>());
+        static_for<B + 1, E>(f);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ __forceinline__ void pp_signal(int *red, int c)
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if ((threadIdx.x & 63) == 0) __atomic_fetch_add(&red[c], 1, __ATOMIC_RELAXED);
 }
 
 struct PPSlots {
@@ -216,7 +204,7 @@ __device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots &s
 __device__ __forceinline__ void pp_account(const DecodeArgs &a, const PPSlots &s, int grp, int (&sums)[6],
                                            unsigned *redo, unsigned long long *acc)
 {
-    block_sum_n<6>(sums, s.red + 32);
+    block_sum_n<6>(sums, s.red + kPPRedSums);
     if (threadIdx.x == 0) {
 #pragma unroll
         for (int X = 0; X < 2; ++X) {
@@ -240,38 +228,42 @@ __device__ __forceinline__ void pp_account(const DecodeArgs &a, const PPSlots &s
     }
 }
 
-// ---- one wave's work: R check rows of each slot and, with HB, CPT bit slots ----
-// Row r of thread t is row-schedule row t + 512 r. The split is per wave (an
-// SGPR branch in the kernel): MODE 0 gives waves 0-7 rows t, t + 512 (R = 2)
-// and waves 8-15 the bit slots of schedule thread t - 512 (HB); MODE 1 gives
-// every thread its row t (R = 1) and waves 8-15 also the bit slots, so the
-// check rows spread over 4 waves per SIMD with one row each.
-template <int SRC, int DC, int CPT, int VAR, bool FDIV, int R, bool HB, bool SYNC>
+// ---- one wave's work: R check rows of each slot, or (HB) CPT bit slots ----
+// The split is per wave (an SGPR branch in the kernel): waves 0-7 hold rows t
+// and t + 512 of the row schedule (R = 2), waves 8-15 the bit slots of schedule
+// thread t - 512 (HB, R = 0). Row r runs a check node of compile-time degree
+// DC0 (r = 0) or DC1 (r = 1): with the degree-aware slots (graph.h pp_row_slots)
+// the younger check wave of each SIMD -- the SQ issues oldest-first, so it sets
+// the interval -- holds only rows of degree <= 7 (DC0 = DC1 = 7) and the older
+// one the degree-8 rows and the padding in its row 1 (DC1 = 8). A row of lower
+// degree than its DC has padding edges: +inf gathers (no effect on min, sign or
+// argmin) and scatters to the lane's dummy slot.
+template <int SRC, int DC0, int DC1, int CPT, int VAR, bool FDIV, int R, bool HB>
 __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, const RowSched &rs, const PPSlots &s,
                                         unsigned *redo, unsigned long long *acc)
 {
     using P = Pack<double, 1>;
+    constexpr int DCX = 8;                    // schedule stride (rs.dc)
     constexpr int RR = R > 0 ? R : 1;   // array extents
+    static_assert(DC0 <= DCX && DC1 <= DCX && (R == 0) == HB, "pp_role shape");
     const int tid = threadIdx.x, N = g.N, lane = tid & 63;
     // check rows: schedule, and the c2v each sent last iteration, per slot
+    // (entries past a row's DC are never touched, so they take no registers)
     [[maybe_unused]] int deg[RR];
-    [[maybe_unused]] uint32_t colw[RR][DC / 2], posw[RR][DC / 2];
-    [[maybe_unused]] P prev[2][RR][DC];
+    [[maybe_unused]] uint32_t colw[RR][DCX / 2], posw[RR][DCX / 2];
+    [[maybe_unused]] P prev[2][RR][DCX];
     if constexpr (R > 0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int j = tid + r * kPPRole;
             deg[r] = rs.cn_deg[j];
-#pragma unroll
-            for (int q = 0; q < DC / 8; ++q) {
-                const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)j * DC)[q];
-                const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)j * DC)[q];
-                colw[r][4 * q + 0] = xc.x; colw[r][4 * q + 1] = xc.y; colw[r][4 * q + 2] = xc.z; colw[r][4 * q + 3] = xc.w;
-                posw[r][4 * q + 0] = xp.x; posw[r][4 * q + 1] = xp.y; posw[r][4 * q + 2] = xp.z; posw[r][4 * q + 3] = xp.w;
-            }
+            const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)j * DCX)[0];
+            const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)j * DCX)[0];
+            colw[r][0] = xc.x; colw[r][1] = xc.y; colw[r][2] = xc.z; colw[r][3] = xc.w;
+            posw[r][0] = xp.x; posw[r][1] = xp.y; posw[r][2] = xp.z; posw[r][3] = xp.w;
             if (deg[r] == 0)   // rows past M: gather the +0 entry, so their messages stay 0
 #pragma unroll
-                for (int q = 0; q < DC / 2; ++q) colw[r][q] = (uint32_t)(N + 2) * 0x10001u;
+                for (int q = 0; q < DCX / 2; ++q) colw[r][q] = (uint32_t)(N + 2) * 0x10001u;
         }
     }
     // bit slots of schedule thread bt
@@ -310,7 +302,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) prev[X][r][k].v[0] = 0.0;
+                    for (int k = 0; k < DCX; ++k) prev[X][r][k].v[0] = 0.0;
         }
         if constexpr (HB) {
 #pragma unroll
@@ -329,29 +321,27 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
             if (tid == kPPRole) s.app[0][N].v[0] = s.app[1][N].v[0] = __builtin_huge_val();
             if (tid == kPPRole + 1) s.app[0][N + 2].v[0] = s.app[1][N + 2].v[0] = 0.0;
         }
-        if (SYNC && tid == 0)
-#pragma unroll
-            for (int q = kPPCheckDone; q < kPPBitDone + 2; ++q) s.red[q] = 0;
         __syncthreads();   // B2: yq in app
 
         // One barrier interval: the rows of slot X (their reads first), the bit
         // nodes of slot 1 - X when `bits` (HB waves), then the rows' check nodes.
         auto interval = [&](auto Xc, bool rows, bool bits) {
             constexpr int X = decltype(Xc)::value, Y = 1 - X;
-            [[maybe_unused]] P xin[RR][DC];
+            [[maybe_unused]] P xin[RR][DCX];
             if constexpr (R > 0) {
                 if (rows && LDPC_PP_EXP != 2) {
 #pragma unroll
                     for (int r = 0; r < R; ++r)
 #pragma unroll
-                        for (int q = 0; q < DC / 2; ++q) asm volatile("" : "+v"(colw[r][q]), "+v"(posw[r][q]));
+                        for (int q = 0; q < DCX / 2; ++q) asm volatile("" : "+v"(colw[r][q]), "+v"(posw[r][q]));
                     const uint32_t ab = s.app_base[X];
+                    static_for<0, (LDPC_PP_PREFETCH ? R : 1)>([&](auto rc) {
+                        constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
 #pragma unroll
-                    for (int r = 0; r < (LDPC_PP_PREFETCH ? R : 1); ++r)
-#pragma unroll
-                        for (int k = 0; k < DC; ++k)
+                        for (int k = 0; k < DCr; ++k)
                             xin[r][k] = lds_at<P>((LDPC_PP_EXP == 5 || LDPC_PP_EXP == 7) ? ab + 8u * (uint32_t)(lane + 64 * (k + 8 * r))
-                                                                                         : addr8<DC>(colw[r], k, ab));
+                                                                                         : addr8<DCX>(colw[r], k, ab));
+                    });
                 }
             }
             if constexpr (HB) {
@@ -372,66 +362,42 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
             if constexpr (R > 0) {
                 if (rows && LDPC_PP_EXP != 2) {
                     const uint32_t ab = s.app_base[X], cb = s.c2v_base[X];
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
+                    static_for<0, R>([&](auto rc) {
+                        constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
                         if (!LDPC_PP_PREFETCH && r > 0) {
 #pragma unroll
-                            for (int k = 0; k < DC; ++k) xin[r][k] = lds_at<P>(addr8<DC>(colw[r], k, ab));
+                            for (int k = 0; k < DCr; ++k) xin[r][k] = lds_at<P>(addr8<DCX>(colw[r], k, ab));
                         }
                         bool ok = true;
                         if constexpr (LDPC_PP_EXP == 3) {
 #pragma unroll
-                            for (int k = 0; k < DC; ++k) prev[X][r][k].v[0] = xin[r][k].v[0] - prev[X][r][k].v[0];
+                            for (int k = 0; k < DCr; ++k) prev[X][r][k].v[0] = xin[r][k].v[0] - prev[X][r][k].v[0];
                         } else {
-                            ok = cn_fast64<DC, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta);
+                            ok = cn_fast64<DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta);
                         }
                         if (!ok && deg[r] > 0 && LDPC_PP_EXP == 0) s.red[X] = 1;   // experiments: never re-decode
                         if constexpr (LDPC_PP_EXP != 4) {
 #pragma unroll
-                            for (int k = 0; k < DC; ++k)
+                            for (int k = 0; k < DCr; ++k)
                                 lds_put<P>((LDPC_PP_EXP == 6 || LDPC_PP_EXP == 7)
                                                ? cb + 8u * (uint32_t)(lane + 64 * ((k + 8 * r + 16 * (tid >> 6)) % 112))
-                                               : addr8<DC>(posw[r], k, cb),
+                                               : addr8<DCX>(posw[r], k, cb),
                                            prev[X][r][k]);
                         }
                         if (R > 1 && LDPC_PP_ROWFENCE) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
-                    }
+                    });
                 }
             }
         };
-        if constexpr (SYNC) {
-            // check(X, it) after bit(X, it-1) of all 8 bit waves; bit(X, it) after check(X, it)
-            static_assert(R == 0 || !HB, "dataflow sync: a wave holds rows or bit slots");
-            constexpr int W = kPPRole / 64;
-            for (int it = 0; it < a.T; ++it) {
-                if constexpr (R > 0) {
-                    pp_wait(s.red, kPPBitDone + 0, W * it);
-                    interval(std::integral_constant<int, 0>(), true, false);
-                    pp_signal(s.red, kPPCheckDone + 0);
-                    pp_wait(s.red, kPPBitDone + 1, W * it);
-                    interval(std::integral_constant<int, 1>(), true, false);
-                    pp_signal(s.red, kPPCheckDone + 1);
-                } else {
-                    pp_wait(s.red, kPPCheckDone + 0, W * (it + 1));
-                    interval(std::integral_constant<int, 1>(), false, true);   // bits of slot 0
-                    pp_signal(s.red, kPPBitDone + 0);
-                    pp_wait(s.red, kPPCheckDone + 1, W * (it + 1));
-                    interval(std::integral_constant<int, 0>(), false, true);   // bits of slot 1
-                    pp_signal(s.red, kPPBitDone + 1);
-                }
-            }
-            __syncthreads();
-        } else {
-            for (int it = 0; it < a.T; ++it) {
-                interval(std::integral_constant<int, 0>(), true, it > 0);
-                PP_BARRIER();   // | check(0,it) | bit(1,it-1) |
-                interval(std::integral_constant<int, 1>(), true, true);
-                PP_BARRIER();   // | check(1,it) | bit(0,it) |
-            }
-            if (a.T > 0) {
-                interval(std::integral_constant<int, 0>(), false, true);
-                PP_BARRIER();   // | -- | bit(1,T-1) |
-            }
+        for (int it = 0; it < a.T; ++it) {
+            interval(std::integral_constant<int, 0>(), true, it > 0);
+            PP_BARRIER();   // | check(0,it) | bit(1,it-1) |
+            interval(std::integral_constant<int, 1>(), true, true);
+            PP_BARRIER();   // | check(1,it) | bit(0,it) |
+        }
+        if (a.T > 0) {
+            interval(std::integral_constant<int, 0>(), false, true);
+            PP_BARRIER();   // | -- | bit(1,T-1) |
         }
 
         // syndrome (rows; padding edges read +inf: parity 0; rows past M skipped) and
@@ -441,13 +407,13 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
         for (int X = 0; X < 2; ++X) {
             if constexpr (R > 0) {
                 int synd = 0;
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
+                static_for<0, R>([&](auto rc) {
+                    constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
                     int par = 0;
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) par ^= (s.app[X][u16_at<DC>(colw[r], k)].v[0] > 0.0) ? 0 : 1;
+                    for (int k = 0; k < DCr; ++k) par ^= (s.app[X][u16_at<DCX>(colw[r], k)].v[0] > 0.0) ? 0 : 1;
                     synd |= deg[r] > 0 ? par : 0;
-                }
+                });
                 sums[3 * X + 2] = synd;
             }
             if constexpr (HB) {
@@ -479,41 +445,76 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
 
 }  // namespace
 
-#ifndef LDPC_PP_MODE
-#define LDPC_PP_MODE 0
-#endif
 // Experiments: s_nop instructions at the kernel entry shift the code that follows by 4 bytes
 // each (the code-layout sensitivity of the loops, with and without -falign-loops).
 #ifndef LDPC_PP_ENTRY_NOPS
 #define LDPC_PP_ENTRY_NOPS 0
 #endif
+// Code order of the roles (experiments): 0 bit role first, 1 check roles first (younger
+// before older), 2 check roles first (older before younger).
+#ifndef LDPC_PP_ROLEORDER
+#define LDPC_PP_ROLEORDER 0
+#endif
 
-template <int SRC, int DC, int CPT, int VAR, bool FDIV, int MODE>
+// SPLIT: the schedule has degree-aware row slots (rs.dc_low == 7, graph.h
+// pp_row_slots): check waves 4-7 run two 7-edge rows, waves 0-3 a 7-edge and an
+// 8-edge row. Otherwise every row runs the 8-edge check node.
+template <int SRC, int CPT, int VAR, bool FDIV, bool SPLIT>
 __global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph g, RowSched rs, unsigned *redo)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #pragma unroll
     for (int i = 0; i < LDPC_PP_ENTRY_NOPS; ++i) asm volatile("s_nop 0");
     const PPSlots s = pp_slots(smem, g.N, rs.e_pad + 64);
-    unsigned long long *acc = reinterpret_cast<unsigned long long *>(s.red + 128);   // thread 0's block totals
+    unsigned long long *acc = reinterpret_cast<unsigned long long *>(s.red + kPPRedAcc);   // thread 0's block totals
     if (threadIdx.x == 0) {
-        s.red[0] = s.red[1] = s.red[kPPSyncAbort] = 0;
+        s.red[0] = s.red[1] = 0;
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
     }
     // the split is wave-uniform (an SGPR branch), so every wave meets every barrier
-    const bool low = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < kPPRole / 64;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool low = wave < kPPRole / 64;
     if (LDPC_PP_PRIO == 1 && low) __builtin_amdgcn_s_setprio(1);
     if (LDPC_PP_PRIO == 2 && !low) __builtin_amdgcn_s_setprio(1);
     if (LDPC_PP_PRIO == 3 && ((threadIdx.x >> 8) & 1)) __builtin_amdgcn_s_setprio(1);
-    if constexpr (MODE == 1) {
-        if (low) pp_role<SRC, DC, CPT, VAR, FDIV, 1, false, false>(a, g, rs, s, redo, acc);
-        else pp_role<SRC, DC, CPT, VAR, FDIV, 1, true, false>(a, g, rs, s, redo, acc);
-    } else {   // 0: barrier intervals, 2: dataflow counters
-        if (low) pp_role<SRC, DC, CPT, VAR, FDIV, 2, false, MODE == 2>(a, g, rs, s, redo, acc);
-        else pp_role<SRC, DC, CPT, VAR, FDIV, 0, true, MODE == 2>(a, g, rs, s, redo, acc);
+    if (LDPC_PP_PRIO == 4 && low && wave >= kPPRole / 128) __builtin_amdgcn_s_setprio(1);
+    if (LDPC_PP_PRIO == 5 && low) {
+        if (wave >= kPPRole / 128) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
     }
-    if (MODE == 2 && threadIdx.x == 0 && s.red[kPPSyncAbort]) atomicAdd(&a.counts[7], 1ull);   // host: error
+#if LDPC_PP_ROLEORDER == 0
+    if (!low)
+        pp_role<SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
+    else if (!SPLIT)
+        pp_role<SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+    else if (wave >= kPPRole / 128)
+        pp_role<SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+    else
+        pp_role<SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+#elif LDPC_PP_ROLEORDER == 1
+    if (low) {
+        if (!SPLIT)
+            pp_role<SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+        else if (wave >= kPPRole / 128)
+            pp_role<SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+        else
+            pp_role<SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+    } else {
+        pp_role<SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
+    }
+#else
+    if (low) {
+        if (!SPLIT)
+            pp_role<SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+        else if (wave < kPPRole / 128)
+            pp_role<SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+        else
+            pp_role<SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+    } else {
+        pp_role<SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
+    }
+#endif
     if (threadIdx.x == 0 && acc[3] > 0) {
         acc[4] = acc[3] * (unsigned long long)a.T;
 #pragma unroll
@@ -528,17 +529,15 @@ int rows_pp_lds_bytes(const DevGraph &g, const RowSched &rs)
 
 bool rows_pp_supported(const DevGraph &g, const RowSched &rs)
 {
-    return rs.threads == kPPRole && rs.rpt == 2 && rs.cpt == 4 && rs.dc == 8 && g.N + 3 <= 0xffff &&
-           rows_pp_lds_bytes(g, rs) <= 160 * 1024;
+    return rs.threads == kPPRole && rs.rpt == 2 && rs.cpt == 4 && rs.dc == 8 && (rs.dc_low == 0 || rs.dc_low == 7) &&
+           g.N + 3 <= 0xffff && rows_pp_lds_bytes(g, rs) <= 160 * 1024;
 }
 
 template <int SRC, int VAR, bool FDIV>
 static hipError_t launch_pp_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, unsigned *redo,
                               hipStream_t s, int num_cus)
 {
-    const int mode = std::getenv("LDPC_PP_MODE") ? std::atoi(std::getenv("LDPC_PP_MODE")) : LDPC_PP_MODE;
-    auto fn = mode == 1 ? k_rows_pp<SRC, 8, 4, VAR, FDIV, 1>
-              : mode == 2 ? k_rows_pp<SRC, 8, 4, VAR, FDIV, 2> : k_rows_pp<SRC, 8, 4, VAR, FDIV, 0>;
+    auto fn = rs.dc_low == 7 ? k_rows_pp<SRC, 4, VAR, FDIV, true> : k_rows_pp<SRC, 4, VAR, FDIV, false>;
     const int lds = rows_pp_lds_bytes(g, rs);
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;

@@ -18,6 +18,7 @@ reported totals equal a frame-by-frame run of the same noise.
 from __future__ import annotations
 
 import math
+import time
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
@@ -155,7 +156,8 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
                    max_frames: Optional[int] = None, exact_stop: bool = True, device=None,
                    iters_in_frames: bool = False, launcher=None, first_round: Optional[int] = None,
                    resume: Optional[PointState] = None,
-                   on_round: Optional[Callable[[PointState], None]] = None) -> PointResult:
+                   on_round: Optional[Callable[[PointState], None]] = None,
+                   on_round_interval: float = 0.0) -> PointResult:
     """Run one SNR point to the reference's stop rule.
 
     run_batch(first_cw, n) must decode global frames first_cw..first_cw+n-1 on
@@ -175,10 +177,14 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
     global index and a round launched ahead of the stop is discarded.
 
     resume: start from a checkpointed PointState (the same on every rank) instead
-    of frame 0. on_round(state): called on every rank after each fully counted
+    of frame 0. on_round(state): called on every rank after a fully counted
     round with the point's state (its histogram all-reduced: a collective), for
-    checkpoints."""
+    checkpoints -- after every round, or (on_round_interval > 0 s) after the first
+    round that ends at least that long after the previous call. Rank 0's clock
+    decides, and its decision rides in the round's counter all-reduce, so every
+    rank makes the same call without another collective."""
     comm = _Comm(device)
+    t_saved = time.monotonic()
     acc = np.zeros(6, dtype=np.int64)
     res = PointResult(ebn0_db, N, T)
     hist_local = np.zeros(N, dtype=np.int64)   # rounds fully counted: this rank's frames
@@ -229,9 +235,13 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
                 launcher.launch((rnd + 1) % 2, first_of(rnd + 1), size_of(rnd + 1))
             fr = np.ascontiguousarray(launcher.collect(rnd % 2))
         raw = fr.view(np.int32).reshape(-1, 4)
+        want_save = on_round is not None and comm.rank == 0 and \
+            (on_round_interval <= 0 or time.monotonic() - t_saved >= on_round_interval)
         local = np.array([raw[:, 0].sum(), (raw[:, 0] > 0).sum(), raw[:, 1].sum(), len(raw),
-                          raw[:, 3].sum() if iters_in_frames else T * len(raw), raw[:, 2].sum()], dtype=np.int64)
-        tot = comm.allreduce_sum(local)
+                          raw[:, 3].sum() if iters_in_frames else T * len(raw), raw[:, 2].sum(),
+                          int(want_save)], dtype=np.int64)
+        tot7 = comm.allreduce_sum(local)
+        tot, save = tot7[:6], tot7[6] > 0
         decoded += int(tot[3])
         last = tot
         after = acc + tot
@@ -248,7 +258,8 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
             acc = after
             w = raw[:, 0]
             np.add.at(hist_local, w[w > 0] - 1, 1)
-            if on_round is not None:
+            if on_round is not None and save:
+                t_saved = time.monotonic()
                 on_round(PointState(starts[rnd] + size_of(rnd) * comm.world, acc.copy(),
                                     comm.allreduce_sum(hist_local) + hist_base, rounds0 + rnd + 1, decoded))
         rnd += 1

@@ -21,8 +21,8 @@ line for each point.
 Log line: SNR BER avgIt FER T [Ymax] [alpha] [delta] alist (EMS: SNR BER avgIt FER T nm offset alist;
 BER over coded bits, 4 per GF(16) symbol).
 
---checkpoint FILE appends each point's running totals after every round
-(checkpoint.py); a sweep restarted with the same FILE and settings takes the
+--checkpoint FILE appends each point's running totals after a round at most
+every --checkpoint-interval seconds (default 10; 0 = every round; checkpoint.py); a sweep restarted with the same FILE and settings takes the
 seed from it, skips finished points and resumes the others at their next
 frame, with the totals an uninterrupted run gives.
 """
@@ -79,6 +79,9 @@ def parse(argv=None):
                    help="every rank on device 0 (rehearsal of N ranks on one GPU, with --backend gloo)")
     p.add_argument("--checkpoint", metavar="FILE",
                    help="per-round progress file (.partial); an existing one is resumed (same settings)")
+    p.add_argument("--checkpoint-interval", type=float, default=10.0, metavar="S",
+                   help="seconds between checkpoint records (0 = after every round); each record "
+                        "all-reduces the point's error-weight histogram")
     return p.parse_args(argv)
 
 
@@ -187,7 +190,8 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         res = sim.simulate_point(run_batch, g.N, a.iterations, snr, a.batch, a.min_bit_errors,
                                  min_fe, a.max_frames, device=device, launcher=launcher, first_round=a.first_round,
-                                 resume=resume, on_round=on_round)
+                                 resume=resume, on_round=on_round,
+                                 on_round_interval=a.checkpoint_interval)
         dt = time.perf_counter() - t0
         c = res.counts
         ran = c["frames"] - (int(resume.acc[3]) if resume else 0)   # frames counted by this run
@@ -219,7 +223,8 @@ def _ems_sweep(a, seed, world, rank, device, ck=None) -> int:
         res = sim.simulate_point(run_batch, bits, a.iterations, snr, a.batch, a.min_bit_errors,
                                  a.min_frame_errors if a.min_frame_errors is not None else 40, a.max_frames,
                                  device=device, iters_in_frames=True, first_round=a.first_round,
-                                 resume=resume, on_round=on_round)
+                                 resume=resume, on_round=on_round,
+                                 on_round_interval=a.checkpoint_interval)
         dt = time.perf_counter() - t0
         c = res.counts
         ran = c["frames"] - (int(resume.acc[3]) if resume else 0)   # frames counted by this run

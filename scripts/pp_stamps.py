@@ -10,8 +10,9 @@ iv = float(sys.argv[2])
 for i, l in enumerate(a):
     s = l[: 256 * 16 * 2].reshape(256, 16, 2).astype(np.float64)
     used = s[s[:, :, 0].sum(axis=1) > 0]
-    for name, w in (("check", slice(0, 8)), ("bit", slice(8, 16))):
+    for name, w in (("check 0-3", slice(0, 4)), ("check 4-7", slice(4, 8)), ("bit 8-11", slice(8, 12)),
+                    ("bit 12-15", slice(12, 16))):
         work = used[:, w, 0] / iv
         wait = used[:, w, 1] / iv
-        print(f"launch {i} {name:5s}: blocks={len(used)} work {work.mean():7.1f} (min {work.min():7.1f} max "
+        print(f"launch {i} {name:9s}: blocks={len(used)} work {work.mean():7.1f} (min {work.min():7.1f} max "
               f"{work.max():7.1f})  wait {wait.mean():7.1f}  cycles/interval")

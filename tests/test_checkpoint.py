@@ -99,3 +99,27 @@ def test_torn_last_record_is_ignored(tmp_path):
     st = ck.point_state(0, 1.5, N)
     assert st is not None and st.rounds == 2 and st.next_frame == 2 * 97
     assert int((st.hist * np.arange(1, N + 1)).sum()) == int(st.acc[0])
+
+
+@pytest.mark.parametrize("tail", ['{"kind": "round", "k": 0, "snr": 1.5, "next_fr', None])
+def test_torn_tail_repaired_before_resume_appends(tmp_path, tail):
+    """A sweep killed mid-write (torn last record), or one whose last complete record lost
+    its newline, resumes, appends further rounds, can be killed and resumed again, and ends
+    with the uninterrupted run's log (the first appended record was glued onto
+    the fragment and the next load refused the file)."""
+    ref_dir = tmp_path / "ref"
+    ref_dir.mkdir()
+    _sweep(_args(ref_dir), _point_runner())
+    want = (ref_dir / "log.txt").read_text().splitlines()
+    a = _args(tmp_path)
+    with pytest.raises(_Killed):
+        _sweep(a, _point_runner(2))
+    p = tmp_path / "ck.partial"
+    txt = p.read_text()
+    p.write_text(txt + tail if tail is not None else txt.rstrip("\n"))
+    with pytest.raises(_Killed):
+        _sweep(_args(tmp_path), _point_runner(2))     # resume, append two rounds, killed again
+    recs = [json.loads(l) for l in p.read_text().splitlines()]   # every line parses
+    assert sum(r["kind"] == "round" for r in recs) == 4
+    _sweep(_args(tmp_path), _point_runner())
+    assert (tmp_path / "log.txt").read_text().splitlines() == want

@@ -103,6 +103,21 @@ def test_nb_alist_loader_rejects_inconsistent_views(tmp_path):
     assert (g.N, g.M, g.q, g.E, g.maxdv, g.maxdc) == (1000, 500, 16, 2000, 2, 4)
 
 
+def test_nb_graph_rejects_degree_one_check():
+    """A GF(q) check of degree 1 (or 0) is refused at graph creation (LDPC_ERR_GRAPH),
+    before a context's slot-swizzle search could pick two slots of it."""
+    from ldpcsimulation_amd import native
+    cols = [[(0, 3)], [(0, 5), (1, 7)], [(1, 2)]]
+    rows = [[(1, 5), (0, 3)], [(1, 7), (2, 2)]]
+    g = native.NbGraph.from_lists(3, 2, 16, cols, rows)
+    assert (g.N, g.M, g.maxdc) == (3, 2, 2)
+    bad_cols = [[(0, 3)], [(1, 7)], [(1, 2)]]
+    bad_rows = [[(0, 3)], [(1, 7), (2, 2)]]           # check 0 has one edge
+    with pytest.raises(native.LdpcError) as e:
+        native.NbGraph.from_lists(3, 2, 16, bad_cols, bad_rows)
+    assert e.value.code == -6 and "degree" in str(e.value)
+
+
 def test_ems_q2_equals_binary_min_sum_oracle():
     """GF(2) EMS (nm = 2, no offset, no early stop) is binary min-sum: identical decisions to the
     reference-pinned min-sum oracle on the same bit LLRs (PEGReg504x1008, glibc noise)."""

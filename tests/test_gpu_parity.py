@@ -339,3 +339,34 @@ def test_dvbs2_flood_decisions_vs_oracle(gpu_ctx_factory, prec):
     want = A.decode(y, 6, O.Cfg(variant=1, alpha=1.25))
     assert int((d != want).sum()) == 0
     assert np.array_equal(fr["bit_err"], (want != 1).sum(axis=1))
+
+
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_flood_heavy_column_vs_oracle(tmp_path, monkeypatch, prec):
+    """Phase flooding on a code with a column of degree 40: the packed-message bit
+    phase is built for column degrees <= 32, so such a code takes the
+    c2v-array bit phase (any degree); decisions equal the oracle's."""
+    from ldpcsimulation_amd import codes
+    native = _native()
+    rng = np.random.default_rng(40)
+    N, M = 600, 300
+    rows = [sorted(set(rng.choice(np.arange(1, N), size=6, replace=False).tolist())) for _ in range(M)]
+    for j in range(40):                       # bit 0 in 40 checks
+        rows[j] = sorted(set(rows[j]) | {0})
+    path = str(tmp_path / "heavy_col.alist")
+    codes.write_alist(codes.ParityCheck.from_rows(N, rows), path)
+    monkeypatch.setenv("LDPC_KERNEL", "flood")
+    ctx = native.Context(native.Graph.from_alist(path), 0, 64)
+    f32 = prec == "f32"
+    y = _glibc_frames(N, 16, 3.0, 0.5, seed=41)
+    if f32:
+        y = y.astype(np.float32)
+    A = O.Alist(path)
+    assert sum(0 in r for r in rows) == 40
+    for v in (VARIANTS["ms"], VARIANTS["nms"]):
+        for T in (1, 7):
+            cfg = native.DecoderConfig(T=T, precision=native.F32 if f32 else native.F64, **v)
+            assert ctx.kernel_info(cfg)["kernel"] == "flood"
+            d, fr, cnt = ctx.decode(y, cfg)
+            want = A.decode(y, T, O.Cfg(**v))
+            assert int((d != want).sum()) == 0, (v, T)

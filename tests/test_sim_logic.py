@@ -316,3 +316,94 @@ def test_resume_two_ranks_gloo():
     for nf, acc, h in out[0][3]:
         res = sim.simulate_point(fake_frames, N, T, 1.5, 77, resume=sim.PointState(nf, np.array(acc), np.array(h)))
         assert res.counts == want and np.array_equal(res.hist, hist)
+
+
+# ---- world sizes 1, 2, 4 and 8 ----
+# One spawned process group per world size runs a list of scenarios; every rank
+# must report the sequential run's totals and histogram (decodeMinSum.cpp:189: the
+# stop rule cuts at the same frame for any W), whatever the batch, the first round,
+# the launcher or a resumed state.
+
+def _run_scenario(sc, rank):
+    gen = {"fake": fake_frames, "high": fake_frames_high_fer}[sc["gen"]]
+    st = []
+    interval = sc.get("interval", (0.0, 0.0))
+    res = sim.simulate_point(gen, N, T, 1.5, sc["batch"], first_round=sc.get("first_round"),
+                             launcher=_FakeLauncher() if sc.get("launcher") else None,
+                             resume=sc.get("resume"), on_round=st.append if sc.get("collect") else None,
+                             on_round_interval=interval[0] if rank == 0 else interval[1])
+    return (res.counts, res.hist.tolist(), res.rounds, res.frames_decoded,
+            [(s.next_frame, s.acc.tolist(), s.hist.tolist(), s.rounds, s.frames_decoded) for s in st])
+
+
+def _scenario_worker(rank, world, port, q, scenarios):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, [_run_scenario(sc, rank) for sc in scenarios]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _ranks(world, scenarios):
+    """Results per scenario, as a list over ranks (rank order)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scenario_worker, args=(r, world, port, q, scenarios)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return [[out[r][i] for r in range(world)] for i in range(len(scenarios))]
+
+
+SCENARIOS = [
+    dict(gen="fake", batch=16),                              # many small rounds
+    dict(gen="fake", batch=300),                             # uneven batch, adaptive first round min(300, 1024)
+    dict(gen="fake", batch=1000, first_round=7),             # first round 7 per rank, doubling to 1000
+    dict(gen="fake", batch=37, first_round=5, launcher=True),   # rounds launched ahead
+    dict(gen="high", batch=65536),                           # high FER: stops inside the first round
+    dict(gen="fake", batch=50, collect=True),                # per-round states (all-reduced histograms)
+    dict(gen="fake", batch=50, collect=True, interval=(0.0, 1e9)),   # rank 0's clock decides for all
+]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_world_sizes_identical_to_sequential(world):
+    want, hist = sequential()
+    want_high = sequential_of(fake_frames_high_fer)
+    per = _ranks(world, SCENARIOS)
+    for sc, ranks in zip(SCENARIOS, per):
+        for rank, (counts, h, rounds, decoded, states) in enumerate(ranks):
+            if sc["gen"] == "high":
+                assert counts == want_high, (world, rank)
+                assert decoded == min(1024, sc["batch"]) * world   # one adaptive round
+                continue
+            assert counts == want, (world, rank, sc)
+            assert np.array_equal(np.array(h), hist), (world, rank, sc)
+            if sc.get("collect"):
+                assert states == ranks[0][4], (world, rank, sc)     # the same states on every rank
+                assert len(states) == rounds - 1                    # every round but the cut one
+                for nf, acc, sh, _, _ in states:
+                    assert acc[3] == nf and int(np.sum(sh)) == acc[1]
+
+
+def test_checkpoint_w2_resumed_at_w4_and_w1():
+    """A state checkpointed by two ranks resumes on four ranks (and on one) with the
+    uninterrupted run's totals and histogram."""
+    want, hist = sequential()
+    (ranks2,) = _ranks(2, [dict(gen="fake", batch=40, collect=True)])
+    states = ranks2[0][4]
+    assert len(states) >= 3
+    resumes = [sim.PointState(nf, np.array(acc), np.array(h), r, d) for nf, acc, h, r, d in states[1::2]]
+    scen = [dict(gen="fake", batch=b, resume=st) for st in resumes for b in (40, 23)]
+    for world in (4, 1):
+        for sc, ranks in zip(scen, _ranks(world, scen)):
+            for rank, (counts, h, rounds, decoded, _) in enumerate(ranks):
+                assert counts == want and np.array_equal(np.array(h), hist), (world, rank, sc["batch"])
+                assert rounds >= sc["resume"].rounds
