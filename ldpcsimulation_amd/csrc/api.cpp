@@ -543,40 +543,50 @@ static ldpc::KernelChoice select_kernel(const ldpc_ctx *c, bool f64, int schedul
 
 static bool is_layered(const ldpc::KernelChoice &kc) { return kc.name[0] == 'l' && kc.name[1] == 'a'; }
 
-// fp64 row graphs run the fast-path row kernel (rows_fast.hip) plus the exact
-// re-decode of codewords whose premise failed; LDPC_ROWS=old keeps the old one.
-// fp32 keeps the row kernel (its fast->exact hand-over measured 8.78 ms against
-// 10.05 ms for the fp32 pair instance of rows_fast); LDPC_ROWS32=fast
-// selects the latter (MS and verified-reciprocal NMS; a after nms_setup).
-static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
-{
-    const char *env = std::getenv("LDPC_ROWS");
-    if (env && std::strcmp(env, "old") == 0) return false;
-    if (!f64) {
-        const char *e32 = std::getenv("LDPC_ROWS32");
-        if (!(e32 && std::strcmp(e32, "fast") == 0) || !ldpc::rows_fast_f32_ok(a)) return false;
-    }
-    return kc.name[0] == 'r' && c->has_rs && ldpc::rows_fast_supported(c->rs, f64) &&
-           ldpc::redo_lds_bytes(c->dg, f64) <= 160 * 1024;
-}
-
-// fp64 on the fast path: the ping-pong kernel (rows_pp.hip: two codewords per
-// 1024-thread block, check and bit waves overlapped; 14.8 vs 16.2 ms per bench
-// launch) when the row schedule fits it; LDPC_ROWS=fast keeps the one-codeword-
-// per-block k_rows_fast (and LDPC_ROWS=old the row kernel).
-// Its schedule: the degree-aware row slots (graph.h pp_row_slots) when the code
-// admits them, else the row kernel's.
+// The ping-pong kernel's schedule: the degree-aware row slots (graph.h
+// pp_row_slots) when the code admits them, else the row kernel's.
 static const ldpc::RowSched &pp_sched(const ldpc_ctx *c)
 {
     const char *e = std::getenv("LDPC_PP_ROWS");   // tests / A/B: "plain" = the row kernel's slots
     if (e && std::strcmp(e, "plain") == 0) return c->rs;
     return c->has_rs_pp ? c->rs_pp : c->rs;
 }
-static bool use_rows_pp(const ldpc_ctx *c, bool f64)
+
+// Row graphs on the fast path: a kernel holding only the fast check node plus the
+// exact re-decode (k_redo) of the codewords whose premise failed.
+//   fp64: the ping-pong kernel (rows_pp.hip: two codewords per 1024-thread block,
+//         check and bit waves overlapped) when the schedule fits it, else the
+//         one-codeword-per-block k_rows_fast (LDPC_ROWS=fast forces the latter);
+//   fp32: pairs as float2 -- MS and NMS with the verified reciprocal (a after
+//         nms_setup) -- on the ping-pong kernel with LDPC_ROWS32=pp, on the pair
+//         instance of k_rows_fast with LDPC_ROWS32=fast; otherwise the row kernel
+//         (kernels.hip k_decode_rows, fast and exact loops in one).
+// LDPC_ROWS=old keeps the row kernel for both.
+enum class FastKind { none, pp, fast };
+static FastKind fast_kind(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
 {
     const char *env = std::getenv("LDPC_ROWS");
-    if (!f64 || (env && std::strcmp(env, "fast") == 0)) return false;
-    return ldpc::rows_pp_supported(c->dg, pp_sched(c));
+    if (env && std::strcmp(env, "old") == 0) return FastKind::none;
+    if (kc.name[0] != 'r' || !c->has_rs || ldpc::redo_lds_bytes(c->dg, f64) > 160 * 1024) return FastKind::none;
+    const bool pp_ok = ldpc::rows_pp_supported(c->dg, pp_sched(c));
+    if (f64) {
+        if (pp_ok && !(env && std::strcmp(env, "fast") == 0)) return FastKind::pp;
+        return ldpc::rows_fast_supported(c->rs, true) ? FastKind::fast : FastKind::none;
+    }
+    if (!ldpc::rows_fast_f32_ok(a)) return FastKind::none;
+    const char *e32 = std::getenv("LDPC_ROWS32");
+    if (e32 && std::strcmp(e32, "fast") == 0)
+        return ldpc::rows_fast_supported(c->rs, false) ? FastKind::fast : FastKind::none;
+    if (e32 && std::strcmp(e32, "pp") == 0) return pp_ok ? FastKind::pp : FastKind::none;
+    return FastKind::none;
+}
+static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
+{
+    return fast_kind(c, kc, f64, a) != FastKind::none;
+}
+static bool use_rows_pp(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
+{
+    return fast_kind(c, kc, f64, a) == FastKind::pp;
 }
 
 // Flooding of codes beyond LDS: one launch per phase over an Infinity-Cache-
@@ -643,8 +653,8 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
     c->last_fast = fast;
     if (fast) {
         HIP_TRY(hipMemsetAsync(c->redo.p, 0, sizeof(unsigned), c->stream));
-        if (use_rows_pp(c, f64))
-            HIP_TRY(ldpc::launch_rows_pp(c->dg, pp_sched(c), a, (unsigned *)c->redo.p, c->stream, c->num_cus));
+        if (use_rows_pp(c, kc, f64, a))
+            HIP_TRY(ldpc::launch_rows_pp(c->dg, pp_sched(c), a, f64, (unsigned *)c->redo.p, c->stream, c->num_cus));
         else
             HIP_TRY(ldpc::launch_rows_fast(c->dg, c->rs, a, f64, kc.lds_bytes, (unsigned *)c->redo.p, c->stream,
                                            c->num_cus));
@@ -953,7 +963,11 @@ int ldpc_ctx_row_sched_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, int32_t *i
     info[5] = kc.cw_per_block;
     info[6] = kc.lds_bytes;
     info[7] = ldpc::blocks_per_cu(c->dg, f64, kc);
-    if (f64 && use_rows_fast(c, kc, f64, ldpc::DecodeArgs{}) && use_rows_pp(c, f64)) {   // one 1024-thread block per CU
+    ldpc::DecodeArgs a;
+    fill_common(a, c, cfg, 1);
+    rc = nms_setup(c, cfg, a);   // fp32 NMS: whether the verified reciprocal (and so the fast kernels) applies
+    if (rc) return rc;
+    if (use_rows_pp(c, kc, f64, a)) {   // one 1024-thread block per CU
         info[6] = ldpc::rows_pp_lds_bytes(c->dg, pp_sched(c));
         info[7] = 1;
     }
@@ -988,12 +1002,12 @@ int ldpc_ctx_kernel_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, char *name, i
     if (rc) return rc;
     if (name && name_len > 0)
         std::snprintf(name, (size_t)name_len, "%s",
-                      cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64, a) ? (use_rows_pp(c, f64) ? "rows_pp" : "rows_fast")
+                      cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64, a) ? (use_rows_pp(c, kc, f64, a) ? "rows_pp" : "rows_fast")
                                                                                 : kc.name);
     if (lds_bytes) *lds_bytes = kc.lds_bytes;
     if (bpc) *bpc = cfg->variant == LDPC_BP ? 0 : is_layered(kc) ? (kc.lds_bytes ? 0 : ldpc::layered_blocks_per_cu(f64, kc))
                                    : ldpc::blocks_per_cu(c->dg, f64, kc);
-    if (cfg->variant != LDPC_BP && use_rows_fast(c, kc, f64, a) && use_rows_pp(c, f64)) {
+    if (cfg->variant != LDPC_BP && use_rows_pp(c, kc, f64, a)) {
         if (lds_bytes) *lds_bytes = ldpc::rows_pp_lds_bytes(c->dg, pp_sched(c));
         if (bpc) *bpc = 1;
     }

@@ -141,13 +141,15 @@ size_t redo_lds_bytes(const DevGraph &g, bool f64);
 hipError_t launch_redo(const DevGraph &g, const DecodeArgs &a, bool f64, const unsigned *redo, hipStream_t s,
                        int num_cus);
 
-// Ping-pong fp64 row kernel (rows_pp.hip): two codewords per 1024-thread
-// block, check waves and bit waves overlapped (same schedule rs as the row
-// kernel: 512 threads, 2 rows and 4 bit slots each, dc 8); redo as above.
+// Ping-pong row kernel (rows_pp.hip): two slots per 1024-thread block -- an
+// fp64 codeword or an fp32 pair (float2) each -- check waves and bit waves
+// overlapped (schedule: 512 threads, 2 rows and 4 bit slots each, dc 8, the
+// degree-aware row slots when rs.dc_low == 7); redo as above (fp32: MS and NMS
+// with the verified reciprocal, rows_fast_f32_ok).
 bool rows_pp_supported(const DevGraph &g, const RowSched &rs);
 int rows_pp_lds_bytes(const DevGraph &g, const RowSched &rs);
-hipError_t launch_rows_pp(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, unsigned *redo, hipStream_t s,
-                          int num_cus);
+hipError_t launch_rows_pp(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, bool f64, unsigned *redo,
+                          hipStream_t s, int num_cus);
 
 // Row-kernel template bounds (host picks the smallest that fits).
 constexpr int kRowsMaxThreads = 1024;

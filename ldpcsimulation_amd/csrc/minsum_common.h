@@ -184,10 +184,12 @@ __device__ __forceinline__ void vn_phases(const Pack<F, C> *c2v, const int (&bas
 // are always committed; the return value is false when one of them reaches
 // 1e30 (or is inf), and the caller hands the block to the exact path before
 // the next iteration (keeping the premise true).
-template <int DC, int C>
-__device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DC], Pack<float, C> (&pv)[DC], bool nms,
+// Edges [0, DC) of arrays of extent DCA >= DC (the entries past DC are not touched).
+template <int DC, int C, int DCA = DC>
+__device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DCA], Pack<float, C> (&pv)[DCA], bool nms,
                                         float alpha, float rcp)
 {
+    static_assert(DC >= 1 && DC <= DCA, "cn_fast degree");
     constexpr uint32_t SIGN = 0x80000000u;
     using V = float __attribute__((ext_vector_type(C)));   // C = 2: one v_pk_add_f32 per edge
     V x[DC];

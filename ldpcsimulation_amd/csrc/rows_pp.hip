@@ -1,6 +1,9 @@
-// rows_pp.hip -- the fp64 headline kernel: flooding min-sum (src/decodeMinSum.cpp
+// rows_pp.hip -- the headline kernel: flooding min-sum (src/decodeMinSum.cpp
 // :247-263, check node :410-450, normalisation :494-515, bit node :452-476)
-// with check and bit work of two codewords overlapped in one workgroup.
+// with check and bit work of two codeword slots overlapped in one workgroup.
+// A slot holds one fp64 codeword (the reference's arithmetic) or an fp32 pair
+// interleaved as float2 (the fp32 throughput path): the same 8-byte LDS words,
+// schedule and roles either way.
 //
 // k_rows_fast (rows_fast.hip) decodes one codeword per 512-thread block; inside
 // a block the check phase (VALU-heavy: the f64 tournament, division, selects)
@@ -27,9 +30,9 @@
 // registers (prev: 2 slots x rows x 8 edges); re-reading it from the row's own
 // c2v slots instead (8 more ds_read_b64 per row) measured slower (16.9 vs 14.7 ms).
 //
-// Premise failures (fast64.h): the slot's flag is raised and the codeword is
-// re-decoded on the exact path (k_redo) after the launch; the other slot of
-// the pair is unaffected. Rows past M (degree 0) gather app[N + 2] = +0, so
+// Premise failures (fast64.h for fp64, minsum_common.h cn_fast for fp32): the
+// slot's flag is raised and its codeword(s) are re-decoded on the exact path
+// (k_redo) after the launch; the other slot is unaffected. Rows past M (degree 0) gather app[N + 2] = +0, so
 // their messages stay 0 (their scatters land in per-lane dummy slots that the
 // padding edges of real rows also use; those read +inf - finite = +inf).
 #include "kernels.h"
@@ -100,10 +103,11 @@ namespace {
 
 constexpr int kPPRole = 512;          // threads per role
 constexpr int kPPWaves = 2 * kPPRole / 64;
-constexpr int kPPRedSums = 32;        // red[] ints: [0,2) slot flags, [32,128) block sums, [128,140) acc (6 x u64)
-constexpr int kPPRedAcc = 128;
-constexpr int kPPRedInts = 160;
-static_assert(kPPRedSums + kPPWaves * 6 <= kPPRedAcc, "block sums overlap acc");
+constexpr int kPPMaxCw = 4;           // codewords per block step (2 slots x an fp32 pair)
+// red[] ints: [0,2) slot flags, [32, 32 + 16 waves x 3 x 4 codewords) block sums, then acc (6 x u64)
+constexpr int kPPRedSums = 32;
+constexpr int kPPRedAcc = kPPRedSums + kPPWaves * 3 * kPPMaxCw;
+constexpr int kPPRedInts = kPPRedAcc + 2 * 6 + 4;
 static_assert(kPPRedAcc % 2 == 0 && kPPRedAcc + 2 * 6 <= kPPRedInts, "acc (6 x u64) outside red[]");
 
 // f(integral_constant<int, I>) for I = B .. E-1: a row loop whose index is a
@@ -117,16 +121,20 @@ __device__ __forceinline__ void static_for(Fn &&f)
     }
 }
 
+template <typename F> struct PPCw { static constexpr int C = sizeof(F) == 8 ? 1 : 2; };   // codewords per slot
+
+template <typename P>
 struct PPSlots {
-    Pack<double, 1> *app[2], *c2v[2];
+    P *app[2], *c2v[2];
     uint32_t app_base[2], c2v_base[2];   // LDS byte addresses
     int *red;
 };
 
-__device__ __forceinline__ PPSlots pp_slots(unsigned char *smem, int N, int EA)
+template <typename P>
+__device__ __forceinline__ PPSlots<P> pp_slots(unsigned char *smem, int N, int EA)
 {
-    using P = Pack<double, 1>;
-    PPSlots s;
+    static_assert(sizeof(P) == 8, "one 8-byte LDS word per slot element");
+    PPSlots<P> s;
     const int SL = N + 3 + EA;
     P *b = reinterpret_cast<P *>(smem);
 #pragma unroll
@@ -140,25 +148,36 @@ __device__ __forceinline__ PPSlots pp_slots(unsigned char *smem, int N, int EA)
     return s;
 }
 
-// Channel of the pair (:214-238) staged into app[X][v] (v < N), by the bit role
-// (threads t0, t0 + nt, ...), 4 bits (one Philox call) per thread and step;
-// unc[X] = this thread's uncoded errors of slot X. The check role stays out of
-// it: with the f64 Box-Muller inlined into its pair loop, the compiler hoisted
-// the channel's loop invariants and spilled 14 doubles per thread around every
-// pair's interval loop (1.2 GB of scratch write-backs per bench launch).
-template <int SRC>
-__device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots &s, int N, int grp, int (&unc)[2],
-                                           int t0, int nt)
+// Channel of the block step's 2C codewords (:214-238) staged into app[X][v].v[c]
+// (v < N; codeword grp*2C + X*C + c), by the bit role (threads t0, t0 + nt, ...),
+// 4 bits (one Philox call) per thread and step; unc[X*C + c] = this thread's
+// uncoded errors. A missing codeword (past the batch) is staged as +1 samples:
+// never a premise break, never counted. The check role stays out of it: with the
+// f64 Box-Muller inlined into its loop, the compiler hoisted the channel's loop
+// invariants and spilled 14 doubles per thread around every interval loop (1.2 GB
+// of scratch write-backs per bench launch).
+template <typename F, int SRC>
+__device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots<Pack<F, PPCw<F>::C>> &s, int N, int grp,
+                                           int (&unc)[2 * PPCw<F>::C], int t0, int nt)
 {
-    using F = double;
-    unc[0] = unc[1] = 0;
+    constexpr int C = PPCw<F>::C;
+#pragma unroll
+    for (int q = 0; q < 2 * C; ++q) unc[q] = 0;
     const int ng4 = (N + 3) / 4;
-    for (int t = t0; t < 2 * ng4; t += nt) {
-        const int X = t >= ng4 ? 1 : 0, g4 = t - X * ng4;
-        const int b = grp * 2 + X;
-        if (b >= a.batch) continue;
+    for (int t = t0; t < 2 * C * ng4; t += nt) {
+        int q = 0;   // codeword of the step (compares, not a division; selects, not a dynamic index)
+#pragma unroll
+        for (int k = 1; k < 2 * C; ++k) q += t >= k * ng4 ? 1 : 0;
+        const int g4 = t - q * ng4, X = q >= C ? 1 : 0, c = q - X * C;
+        const int b = grp * 2 * C + q;
+        auto *ap = X ? s.app[1] : s.app[0];
+        if (b >= a.batch) {
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4)
+                if (4 * g4 + q4 < N) ap[4 * g4 + q4].v[c] = F(1);
+            continue;
+        }
         const uint64_t cw = a.first_cw + (uint64_t)b;
-        Pack<double, 1> *ap = s.app[X];
         F yv[4];
         const int8_t *cvec;
         if (SRC == SRC_GIVEN) {
@@ -183,40 +202,43 @@ __device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots &s
                 if (a.y_out && v < N) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv[q4];
             }
         }
+        int e = 0;
 #pragma unroll
         for (int q4 = 0; q4 < 4; ++q4) {
             const int v = 4 * g4 + q4;
             if (v < N) {
                 const int cv = cvec ? cvec[v] : 1;
-                const F q = front_end<F>(yv[q4], a);
-                ap[v].v[0] = q;
-                const int e = ((q > F(0) ? 1 : -1) * cv < 0);
-                unc[0] += X ? 0 : e;
-                unc[1] += X ? e : 0;
+                const F qv = front_end<F>(yv[q4], a);
+                ap[v].v[c] = qv;
+                e += ((qv > F(0) ? 1 : -1) * cv < 0);
             }
         }
+#pragma unroll
+        for (int qq = 0; qq < 2 * C; ++qq) unc[qq] += qq == q ? e : 0;
     }
 }
 
-// Block sums of the pair's (bit errors, uncoded errors, syndrome) and the
-// per-codeword accounting (:270-288, :382-393) by thread 0; premise failures
-// go to the re-decode list instead.
-__device__ __forceinline__ void pp_account(const DecodeArgs &a, const PPSlots &s, int grp, int (&sums)[6],
-                                           unsigned *redo, unsigned long long *acc)
+// Block sums of the step's (bit errors, uncoded errors, syndrome) per codeword and
+// the per-codeword accounting (:270-288, :382-393) by thread 0; the codewords of a
+// slot whose premise failed go to the re-decode list instead.
+template <int C>
+__device__ __forceinline__ void pp_account(const DecodeArgs &a, int *red, int grp, int (&sums)[6 * C], unsigned *redo,
+                                           unsigned long long *acc)
 {
-    block_sum_n<6>(sums, s.red + kPPRedSums);
+    block_sum_n<6 * C>(sums, red + kPPRedSums);
     if (threadIdx.x == 0) {
+        const int fl[2] = {red[0], red[1]};
+        red[0] = red[1] = 0;   // read once per step; raised again only after the next B1
 #pragma unroll
-        for (int X = 0; X < 2; ++X) {
-            const int b = grp * 2 + X;
+        for (int q = 0; q < 2 * C; ++q) {
+            const int b = grp * 2 * C + q;
             if (b >= a.batch) continue;
-            if (s.red[X]) {
-                s.red[X] = 0;   // read once per pair; raised again only after the next B1
+            if (fl[q / C]) {
                 const unsigned at = atomicAdd(&redo[0], 1u);
                 redo[1 + at] = (unsigned)b;
                 continue;
             }
-            const int w = sums[3 * X], uc = sums[3 * X + 1], sf = sums[3 * X + 2] > 0;
+            const int w = sums[3 * q], uc = sums[3 * q + 1], sf = sums[3 * q + 2] > 0;
             acc[0] += (unsigned long long)w;
             acc[1] += (unsigned long long)(w > 0);
             acc[2] += (unsigned long long)uc;
@@ -226,6 +248,16 @@ __device__ __forceinline__ void pp_account(const DecodeArgs &a, const PPSlots &s
             if (a.frame_res) a.frame_res[b] = make_int4(w, uc, sf, 0);
         }
     }
+}
+
+// The check node of one row: fp64 (fast64.h cn_fast64) or an fp32 pair (cn_fast,
+// MS and NMS with the device-verified reciprocal; VAR picks).
+template <typename F, int DC, int VAR, bool FDIV, int C, int DCA>
+__device__ __forceinline__ bool pp_check_node(const Pack<F, C> (&xin)[DCA], Pack<F, C> (&pv)[DCA], F alpha, F rcp,
+                                              F delta)
+{
+    if constexpr (sizeof(F) == 8) return cn_fast64<DC, VAR, FDIV>(xin, pv, alpha, rcp, delta);
+    else return cn_fast<DC, C>(xin, pv, VAR == V_NMS, alpha, rcp);
 }
 
 // ---- one wave's work: R check rows of each slot, or (HB) CPT bit slots ----
@@ -238,14 +270,18 @@ __device__ __forceinline__ void pp_account(const DecodeArgs &a, const PPSlots &s
 // one the degree-8 rows and the padding in its row 1 (DC1 = 8). A row of lower
 // degree than its DC has padding edges: +inf gathers (no effect on min, sign or
 // argmin) and scatters to the lane's dummy slot.
-template <int SRC, int DC0, int DC1, int CPT, int VAR, bool FDIV, int R, bool HB>
-__device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, const RowSched &rs, const PPSlots &s,
-                                        unsigned *redo, unsigned long long *acc)
+template <typename F, int SRC, int DC0, int DC1, int CPT, int VAR, bool FDIV, int R, bool HB>
+__device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, const RowSched &rs,
+                                        const PPSlots<Pack<F, PPCw<F>::C>> &s, unsigned *redo,
+                                        unsigned long long *acc)
 {
-    using P = Pack<double, 1>;
+    constexpr int C = PPCw<F>::C;
+    using P = Pack<F, C>;
     constexpr int DCX = 8;                    // schedule stride (rs.dc)
     constexpr int RR = R > 0 ? R : 1;   // array extents
     static_assert(DC0 <= DCX && DC1 <= DCX && (R == 0) == HB, "pp_role shape");
+    constexpr bool F64 = sizeof(F) == 8;
+    const F kMax = F64 ? (F)kFast64Max : (F)1e30f;   // premise bound on |yq|
     const int tid = threadIdx.x, N = g.N, lane = tid & 63;
     // check rows: schedule, and the c2v each sent last iteration, per slot
     // (entries past a row's DC are never touched, so they take no registers)
@@ -280,20 +316,25 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
             vgd[i] = __builtin_amdgcn_readfirstlane((int)(info >> 24));
         }
         // padding slots of the bit-node layout hold +0 (adding +0 changes no sum); never written
+        P z;
+#pragma unroll
+        for (int c = 0; c < C; ++c) z.v[c] = F(0);
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
             const int dg = (int)((rs.vn_info[bt * CPT + i] >> 16) & 0xffu);
             const int base = vgb[i] + lane, gd = vgd[i];
-            for (int k = dg; k < gd; ++k) s.c2v[0][base + k * 64].v[0] = s.c2v[1][base + k * 64].v[0] = 0.0;
+            for (int k = dg; k < gd; ++k) s.c2v[0][base + k * 64] = s.c2v[1][base + k * 64] = z;
         }
     }
     auto vdst = [&](int i) -> int { return (int)((vdst2[i / 2] >> (16 * (i & 1))) & 0xffffu); };
-    const double alpha = a.alpha, delta = a.delta, rcp = 1.0 / a.alpha;
-    const int npairs = (a.batch + 1) / 2;
+    const F alpha = (F)a.alpha, delta = (F)a.delta, rcp = F64 ? (F)(1.0 / a.alpha) : (F)a.alpha_rcp;
+    const int nsteps = (a.batch + 2 * C - 1) / (2 * C);
     PP_STAMP_DECL;
-    for (int grp = blockIdx.x; grp < npairs; grp += gridDim.x) {
-        int unc[2] = {0, 0};
-        if constexpr (HB) pp_channel<SRC>(a, s, N, grp, unc, bt, kPPRole);
+    for (int grp = blockIdx.x; grp < nsteps; grp += gridDim.x) {
+        int unc[2 * C];
+#pragma unroll
+        for (int q = 0; q < 2 * C; ++q) unc[q] = 0;
+        if constexpr (HB) pp_channel<F, SRC>(a, s, N, grp, unc, bt, kPPRole);
         __syncthreads();   // B1: channel staged
         [[maybe_unused]] P yq[2][CPT];
         if constexpr (R > 0) {
@@ -302,7 +343,9 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
-                    for (int k = 0; k < DCX; ++k) prev[X][r][k].v[0] = 0.0;
+                    for (int k = 0; k < DCX; ++k)
+#pragma unroll
+                        for (int c = 0; c < C; ++c) prev[X][r][k].v[c] = F(0);
         }
         if constexpr (HB) {
 #pragma unroll
@@ -310,16 +353,26 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                 bool in_ok = true;
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) {
-                    // yq + 0 maps -0 to +0, so app is never -0 (fast64.h premise)
-                    yq[X][i].v[0] = s.app[X][vdst(i) <= N ? vdst(i) : 0].v[0] + 0.0;
-                    in_ok &= __builtin_fabs(yq[X][i].v[0]) < kFast64Max;
+                    const P st = s.app[X][vdst(i) <= N ? vdst(i) : 0];
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        // yq + 0 maps -0 to +0, so app is never -0 (the fast check nodes' premise)
+                        yq[X][i].v[c] = st.v[c] + F(0);
+                        in_ok &= dabs(yq[X][i].v[c]) < kMax;
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) s.app[X][vdst(i)] = yq[X][i];   // v2c = yq on the first pass (:364-370)
                 if (!in_ok) s.red[X] = 1;
             }
-            if (tid == kPPRole) s.app[0][N].v[0] = s.app[1][N].v[0] = __builtin_huge_val();
-            if (tid == kPPRole + 1) s.app[0][N + 2].v[0] = s.app[1][N + 2].v[0] = 0.0;
+            P inf, zero;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                inf.v[c] = dinf<F>();
+                zero.v[c] = F(0);
+            }
+            if (tid == kPPRole) s.app[0][N] = s.app[1][N] = inf;
+            if (tid == kPPRole + 1) s.app[0][N + 2] = s.app[1][N + 2] = zero;
         }
         __syncthreads();   // B2: yq in app
 
@@ -354,7 +407,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                     for (int i = 0; i < CPT; ++i) sum[i] = yq[Y][i];
                     int k = 0;
                     const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-                    vn_phases<double, 1, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum);
+                    vn_phases<F, C, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum);
 #pragma unroll
                     for (int i = 0; i < CPT; ++i) s.app[Y][vdst(i)] = sum[i];
                 }
@@ -371,9 +424,11 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                         bool ok = true;
                         if constexpr (LDPC_PP_EXP == 3) {
 #pragma unroll
-                            for (int k = 0; k < DCr; ++k) prev[X][r][k].v[0] = xin[r][k].v[0] - prev[X][r][k].v[0];
+                            for (int k = 0; k < DCr; ++k)
+#pragma unroll
+                                for (int c = 0; c < C; ++c) prev[X][r][k].v[c] = xin[r][k].v[c] - prev[X][r][k].v[c];
                         } else {
-                            ok = cn_fast64<DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta);
+                            ok = pp_check_node<F, DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta);
                         }
                         if (!ok && deg[r] > 0 && LDPC_PP_EXP == 0) s.red[X] = 1;   // experiments: never re-decode
                         if constexpr (LDPC_PP_EXP != 4) {
@@ -401,44 +456,51 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
         }
 
         // syndrome (rows; padding edges read +inf: parity 0; rows past M skipped) and
-        // decisions / error weight (bit slots; :270, :382-393) of both slots
-        int sums[6] = {0, unc[0], 0, 0, unc[1], 0};
+        // decisions / error weight (bit slots; :270, :382-393) of the step's codewords
+        int sums[6 * C];
 #pragma unroll
         for (int X = 0; X < 2; ++X) {
-            if constexpr (R > 0) {
-                int synd = 0;
-                static_for<0, R>([&](auto rc) {
-                    constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
-                    int par = 0;
 #pragma unroll
-                    for (int k = 0; k < DCr; ++k) par ^= (s.app[X][u16_at<DCX>(colw[r], k)].v[0] > 0.0) ? 0 : 1;
-                    synd |= deg[r] > 0 ? par : 0;
-                });
-                sums[3 * X + 2] = synd;
-            }
-            if constexpr (HB) {
-                const int b = grp * 2 + X;
-                if (b < a.batch) {
-                    const int8_t *cvec =
-                        SRC == SRC_GIVEN ? (a.c ? a.c + (size_t)b * N : nullptr)
-                                         : (a.cw_table ? a.cw_table + (size_t)((a.first_cw + (uint64_t)b) % (uint64_t)a.cw_rows) * N
-                                                       : nullptr);
-                    int w = 0;
+            for (int c = 0; c < C; ++c) {
+                const int q = X * C + c;
+                sums[3 * q] = 0;
+                sums[3 * q + 1] = unc[q];
+                sums[3 * q + 2] = 0;
+                if constexpr (R > 0) {
+                    int synd = 0;
+                    static_for<0, R>([&](auto rc) {
+                        constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
+                        int par = 0;
 #pragma unroll
-                    for (int i = 0; i < CPT; ++i) {
-                        const int v = vdst(i);
-                        if (v < N) {
-                            const int d = s.app[X][v].v[0] > 0.0 ? 1 : -1;   // :471-474
-                            const int cv = cvec ? cvec[v] : 1;
-                            w += (d != cv);
-                            if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+                        for (int k = 0; k < DCr; ++k) par ^= (s.app[X][u16_at<DCX>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
+                        synd |= deg[r] > 0 ? par : 0;
+                    });
+                    sums[3 * q + 2] = synd;
+                }
+                if constexpr (HB) {
+                    const int b = grp * 2 * C + q;
+                    if (b < a.batch) {
+                        const int8_t *cvec =
+                            SRC == SRC_GIVEN ? (a.c ? a.c + (size_t)b * N : nullptr)
+                                             : (a.cw_table ? a.cw_table + (size_t)((a.first_cw + (uint64_t)b) % (uint64_t)a.cw_rows) * N
+                                                           : nullptr);
+                        int w = 0;
+#pragma unroll
+                        for (int i = 0; i < CPT; ++i) {
+                            const int v = vdst(i);
+                            if (v < N) {
+                                const int d = s.app[X][v].v[c] > F(0) ? 1 : -1;   // :471-474
+                                const int cv = cvec ? cvec[v] : 1;
+                                w += (d != cv);
+                                if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+                            }
                         }
+                        sums[3 * q] = w;
                     }
-                    sums[3 * X] = w;
                 }
             }
         }
-        pp_account(a, s, grp, sums, redo, acc);
+        pp_account<C>(a, s.red, grp, sums, redo, acc);
     }
     PP_STAMP_OUT()
 }
@@ -450,22 +512,18 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
 #ifndef LDPC_PP_ENTRY_NOPS
 #define LDPC_PP_ENTRY_NOPS 0
 #endif
-// Code order of the roles (experiments): 0 bit role first, 1 check roles first (younger
-// before older), 2 check roles first (older before younger).
-#ifndef LDPC_PP_ROLEORDER
-#define LDPC_PP_ROLEORDER 0
-#endif
 
 // SPLIT: the schedule has degree-aware row slots (rs.dc_low == 7, graph.h
 // pp_row_slots): check waves 4-7 run two 7-edge rows, waves 0-3 a 7-edge and an
 // 8-edge row. Otherwise every row runs the 8-edge check node.
-template <int SRC, int CPT, int VAR, bool FDIV, bool SPLIT>
+template <typename F, int SRC, int CPT, int VAR, bool FDIV, bool SPLIT>
 __global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph g, RowSched rs, unsigned *redo)
 {
+    using P = Pack<F, PPCw<F>::C>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 #pragma unroll
     for (int i = 0; i < LDPC_PP_ENTRY_NOPS; ++i) asm volatile("s_nop 0");
-    const PPSlots s = pp_slots(smem, g.N, rs.e_pad + 64);
+    const PPSlots<P> s = pp_slots<P>(smem, g.N, rs.e_pad + 64);
     unsigned long long *acc = reinterpret_cast<unsigned long long *>(s.red + kPPRedAcc);   // thread 0's block totals
     if (threadIdx.x == 0) {
         s.red[0] = s.red[1] = 0;
@@ -483,38 +541,14 @@ __global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph 
         if (wave >= kPPRole / 128) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(1);
     }
-#if LDPC_PP_ROLEORDER == 0
     if (!low)
-        pp_role<SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
+        pp_role<F, SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
     else if (!SPLIT)
-        pp_role<SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+        pp_role<F, SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
     else if (wave >= kPPRole / 128)
-        pp_role<SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+        pp_role<F, SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
     else
-        pp_role<SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-#elif LDPC_PP_ROLEORDER == 1
-    if (low) {
-        if (!SPLIT)
-            pp_role<SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-        else if (wave >= kPPRole / 128)
-            pp_role<SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-        else
-            pp_role<SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-    } else {
-        pp_role<SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
-    }
-#else
-    if (low) {
-        if (!SPLIT)
-            pp_role<SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-        else if (wave < kPPRole / 128)
-            pp_role<SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-        else
-            pp_role<SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-    } else {
-        pp_role<SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
-    }
-#endif
+        pp_role<F, SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
     if (threadIdx.x == 0 && acc[3] > 0) {
         acc[4] = acc[3] * (unsigned long long)a.T;
 #pragma unroll
@@ -524,7 +558,7 @@ __global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph 
 
 int rows_pp_lds_bytes(const DevGraph &g, const RowSched &rs)
 {
-    return (int)(2 * (size_t)(g.N + 3 + rs.e_pad + 64) * sizeof(double) + kPPRedInts * sizeof(int));
+    return (int)(2 * (size_t)(g.N + 3 + rs.e_pad + 64) * 8 + kPPRedInts * sizeof(int));
 }
 
 bool rows_pp_supported(const DevGraph &g, const RowSched &rs)
@@ -533,31 +567,37 @@ bool rows_pp_supported(const DevGraph &g, const RowSched &rs)
            g.N + 3 <= 0xffff && rows_pp_lds_bytes(g, rs) <= 160 * 1024;
 }
 
-template <int SRC, int VAR, bool FDIV>
+template <typename F, int SRC, int VAR, bool FDIV>
 static hipError_t launch_pp_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, unsigned *redo,
                               hipStream_t s, int num_cus)
 {
-    auto fn = rs.dc_low == 7 ? k_rows_pp<SRC, 4, VAR, FDIV, true> : k_rows_pp<SRC, 4, VAR, FDIV, false>;
+    auto fn = rs.dc_low == 7 ? k_rows_pp<F, SRC, 4, VAR, FDIV, true> : k_rows_pp<F, SRC, 4, VAR, FDIV, false>;
     const int lds = rows_pp_lds_bytes(g, rs);
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    const int npairs = (a.batch + 1) / 2;
-    const int grid = std::min(num_cus, npairs);
+    constexpr int CW = 2 * PPCw<F>::C;
+    const int nsteps = (a.batch + CW - 1) / CW;
+    const int grid = std::min(num_cus, nsteps);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(2 * kPPRole), lds, s, a, g, rs, redo);
     return hipGetLastError();
 }
 
-hipError_t launch_rows_pp(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, unsigned *redo, hipStream_t s,
-                          int num_cus)
+hipError_t launch_rows_pp(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, bool f64, unsigned *redo,
+                          hipStream_t s, int num_cus)
 {
     if (!rows_pp_supported(g, rs)) return hipErrorInvalidValue;
     const bool given = a.src == SRC_GIVEN;
-#define LDPC_PP_SRC(VARV, FD) \
-    return given ? launch_pp_t<SRC_GIVEN, VARV, FD>(g, rs, a, redo, s, num_cus) : launch_pp_t<SRC_PHILOX, VARV, FD>(g, rs, a, redo, s, num_cus);
-    if (a.variant == V_MS) { LDPC_PP_SRC(V_MS, false) }
-    if (a.variant == V_OMS) { LDPC_PP_SRC(V_OMS, false) }
-    if (markstein_exact_alpha(a.alpha)) { LDPC_PP_SRC(V_NMS, true) }
-    LDPC_PP_SRC(V_NMS, false)
+#define LDPC_PP_SRC(FT, VARV, FD) \
+    return given ? launch_pp_t<FT, SRC_GIVEN, VARV, FD>(g, rs, a, redo, s, num_cus) : launch_pp_t<FT, SRC_PHILOX, VARV, FD>(g, rs, a, redo, s, num_cus);
+    if (!f64) {   // fp32 pairs: MS, or NMS with the verified reciprocal (rows_fast_f32_ok)
+        if (a.variant == V_MS) { LDPC_PP_SRC(float, V_MS, false) }
+        if (a.variant == V_NMS && a.nms_fast) { LDPC_PP_SRC(float, V_NMS, false) }
+        return hipErrorInvalidValue;
+    }
+    if (a.variant == V_MS) { LDPC_PP_SRC(double, V_MS, false) }
+    if (a.variant == V_OMS) { LDPC_PP_SRC(double, V_OMS, false) }
+    if (markstein_exact_alpha(a.alpha)) { LDPC_PP_SRC(double, V_NMS, true) }
+    LDPC_PP_SRC(double, V_NMS, false)
 #undef LDPC_PP_SRC
 }
 

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Ping-pong kernel (rows_pp.hip) against k_rows_fast and the fp64 oracle on the
-bench code: same Philox channel, decisions/per-frame results/counters equal."""
+"""Ping-pong kernel (rows_pp.hip) against the other row kernels and the oracle on the
+bench code: same Philox channel, decisions/per-frame results/counters equal.
+fp64: pp vs k_rows_fast (LDPC_ROWS=fast); fp32 pairs: pp (LDPC_ROWS32=pp) vs the row
+kernel (k_decode_rows, the fp32 default) and the pair instance of k_rows_fast."""
 import os
 import sys
 
@@ -17,21 +19,34 @@ path = codes.ensure_80211n_1944()
 g = native.Graph.from_alist(path)
 ctx = native.Context(g, 0, 4096)
 bad = 0
-for batch, T, vk in ((2048, 50, dict(variant=native.NMS, alpha=1.25)), (257, 7, dict(variant=native.MS)),
-                     (33, 1, dict(variant=native.OMS, delta=0.15)), (5, 0, dict(variant=native.NMS, alpha=1.1))):
-    cfg = native.DecoderConfig(T=T, precision=native.F64, **vk)
-    os.environ["LDPC_ROWS"] = "fast"
-    y0, d0, f0, c0 = ctx.sim_trace(1.5, 0.5, cfg, seed=99, stream_id=3, first_cw=0, batch=batch)
-    os.environ["LDPC_ROWS"] = "pp"
-    assert ctx.kernel_info(cfg)["kernel"] == "rows_pp", ctx.kernel_info(cfg)
-    y1, d1, f1, c1 = ctx.sim_trace(1.5, 0.5, cfg, seed=99, stream_id=3, first_cw=0, batch=batch)
-    ok = np.array_equal(y0, y1) and np.array_equal(d0, d1) and np.array_equal(f0, f1) and c0.as_dict() == c1.as_dict()
-    print(f"batch={batch} T={T} {vk}: pp == fast: {ok}; counts {c1.as_dict()} redo {ctx.redo_count()}", flush=True)
-    if batch <= 257:
-        want = O.Alist(path).decode(y1, T, O.Cfg(**{k: v for k, v in vk.items()}), workers=16)
-        m = int((d1 != want).sum())
-        print(f"   vs oracle: {m} differing decisions", flush=True)
-        bad += m
-    bad += 0 if ok else 1
+CASES = ((2048, 50, dict(variant=native.NMS, alpha=1.25)), (257, 7, dict(variant=native.MS)),
+         (33, 1, dict(variant=native.OMS, delta=0.15)), (5, 0, dict(variant=native.NMS, alpha=1.1)),
+         (4095, 50, dict(variant=native.NMS, alpha=1.25)), (6, 3, dict(variant=native.MS)))
+for prec in (native.F64, native.F32):
+    for batch, T, vk in CASES:
+        cfg = native.DecoderConfig(T=T, precision=prec, **vk)
+        arms = {"f64": [("fast", dict(LDPC_ROWS="fast")), ("pp", {})],
+                "f32": [("rows", {}), ("fast32", dict(LDPC_ROWS32="fast")), ("pp", dict(LDPC_ROWS32="pp"))]}
+        res = {}
+        for name, env in arms["f64" if prec == native.F64 else "f32"]:
+            for k in ("LDPC_ROWS", "LDPC_ROWS32"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            kern = ctx.kernel_info(cfg)["kernel"]
+            res[name] = (kern, ctx.sim_trace(1.5, 0.5, cfg, seed=99, stream_id=3, first_cw=0, batch=batch),
+                         ctx.redo_count())
+        ref_name = next(iter(res))
+        y0, d0, f0, c0 = res[ref_name][1]
+        for name, (kern, (y1, d1, f1, c1), redo) in res.items():
+            ok = np.array_equal(y0, y1) and np.array_equal(d0, d1) and np.array_equal(f0, f1) and \
+                c0.as_dict() == c1.as_dict()
+            print(f"{'f64' if prec == native.F64 else 'f32'} batch={batch} T={T} {vk}: {name} ({kern}) == "
+                  f"{ref_name}: {ok}; redo {redo}", flush=True)
+            bad += 0 if ok else 1
+        if batch <= 257:
+            want = O.Alist(path).decode(y0, T, O.Cfg(**vk), workers=16)
+            m = int((d0 != want).sum())
+            print(f"   vs oracle: {m} differing decisions", flush=True)
+            bad += m
 print("PP_CHECK", "OK" if bad == 0 else f"FAIL {bad}")
 sys.exit(1 if bad else 0)

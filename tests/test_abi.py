@@ -81,17 +81,20 @@ def test_decoder_config_struct_layout():
 
 def test_shipped_library_holds_only_the_kept_ping_pong_kernel():
     """the product library carries only the kept k_rows_pp -- two
-    codewords per block in barrier intervals, instantiated per channel source, variant,
-    division and row-slot layout (k_rows_pp<SRC, CPT, VAR, FDIV, SPLIT>) -- and no
+    slots per block in barrier intervals, instantiated per precision, channel source,
+    variant, division and row-slot layout (k_rows_pp<F, SRC, CPT, VAR, FDIV, SPLIT>) -- and no
     environment switch that swaps in a rejected schedule (the round-3 LDPC_PP_MODE
     1/2 instances: one row per thread, dataflow sync)."""
     import subprocess
     syms = subprocess.run(["nm", "-C", native.LIB_PATH], capture_output=True, text=True, check=True).stdout
     kern = sorted({m for m in re.findall(r"ldpc::k_rows_pp<([^>]*)>", syms)})
-    assert len(kern) == 16, kern                      # 2 sources x (MS, OMS, NMS, NMS Markstein) x 2 layouts
+    # fp64: 2 sources x (MS, OMS, NMS, NMS Markstein) x 2 row-slot layouts;
+    # fp32 pairs: 2 sources x (MS, NMS with the verified reciprocal) x 2 layouts
+    assert len(kern) == 24, kern
     for k in kern:
-        src, cpt, var, fdiv, split = (x.strip() for x in k.split(","))
-        assert cpt == "4" and split in ("true", "false") and src in ("0", "1"), k
+        ft, src, cpt, var, fdiv, split = (x.strip() for x in k.split(","))
+        assert ft in ("double", "float") and cpt == "4" and split in ("true", "false") and src in ("0", "1"), k
+    assert sum(k.startswith("float") for k in kern) == 8
     with open(native.LIB_PATH, "rb") as f:
         blob = f.read()
     assert b"LDPC_PP_MODE" not in blob and b"pp_wait" not in blob
