@@ -57,6 +57,7 @@ import subprocess
 import sys
 import tempfile
 import time
+from typing import Optional
 
 import numpy as np
 
@@ -141,7 +142,7 @@ def pmc_kernel_average(out_dir: str, pattern: str, counter: str):
     return sum(vals.values()) / len(vals) if vals else None
 
 
-def live_traffic(args, kernel: str) -> dict:
+def live_traffic(args, kernel: str, precision: Optional[str] = None) -> dict:
     """HBM bytes per launch of `kernel` in this workload, measured now: one rocprofv3
     --pmc pass per counter (FETCH_SIZE, WRITE_SIZE) over a child bench run (1 warm-up
     + 1 step of the headline, nothing else), each under its own time limit. Per
@@ -152,7 +153,7 @@ def live_traffic(args, kernel: str) -> dict:
         return {"error": "rocprofv3 not on PATH"}
     pattern = KERNEL_SYMBOL.get(kernel, kernel)
     child = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--no-secondary",
-             "--no-cpu-baseline", "--live-pmc", "off", "--precision", args.precision, "--batch", str(args.batch),
+             "--no-cpu-baseline", "--live-pmc", "off", "--precision", precision or args.precision, "--batch", str(args.batch),
              "--T", str(args.T), "--ebn0", str(args.ebn0), "--alpha", str(args.alpha), "--seed", str(args.seed)]
     env = dict(os.environ, TMPDIR="/tmp")
     kib = {}
@@ -511,6 +512,11 @@ def main():
                           "avg_kernel_ms": rs["avg_kernel_ms"], "kernel": rs["kernel"],
                           "lds_frac": rs.get("frac"), "frame_err": int(sec["tot"][1]), "frames": int(sec["tot"][3]),
                           "note": "fp32 throughput path (same workload, Philox stream 1); not the reference's precision"}
+            if args.live_pmc == "auto" and world == 1 and not nested:
+                # the fp32 kernel's HBM bytes, measured the same way as the headline's
+                lt = live_traffic(args, rs["kernel"], "f32")
+                out["f32"]["traffic"] = lt.get("hbm_bytes_per_launch")
+                out["f32"]["traffic_detail"] = {k: v for k, v in lt.items() if k != "hbm_bytes_per_launch"}
         if not args.no_cpu_baseline and world == 1:
             procs = args.cpu_procs or cpu_share()
             try:

@@ -72,9 +72,20 @@ __device__ __forceinline__ double norm64(double m, double alpha, double rcp, dou
 // edges (padding edges read +inf); pv: in = c2v sent last iteration, out = the
 // new c2v. Returns false when the premise may fail for the next iteration (or
 // failed for this one's division).
-template <int DC, int VAR, bool FDIV, int DCA>
+// VALU instructions the scheduler places ahead of each edge's store (ORDER).
+#ifndef LDPC_FAST64_STORE_VALU
+#define LDPC_FAST64_STORE_VALU 3
+#endif
+struct NoSink {
+    __device__ __forceinline__ void operator()(int, const Pack<double, 1> &) const {}
+};
+// sink(k, message) is called as each new message is formed (a store of it, say);
+// with ORDER the scheduler is asked to keep that per-edge order (the selects of
+// edge k, then its store), so the stores start while later edges are computed
+// instead of trailing the whole row.
+template <int DC, int VAR, bool FDIV, int DCA, typename Sink = NoSink, bool ORDER = false>
 __device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DCA], Pack<double, 1> (&pv)[DCA], double alpha,
-                                          double rcp, double delta)
+                                          double rcp, double delta, Sink sink = Sink())
 {
     static_assert(DC >= 1 && DC <= DCA, "cn_fast64 degree");
     constexpr uint32_t SIGN = 0x80000000u;
@@ -119,6 +130,11 @@ __device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DCA], Pac
         const uint32_t h = eq ? s2 : s1, l = eq ? l2 : l1;
         const uint32_t m = (VAR == V_OMS) ? (eq ? mk2 : mk1) : SIGN;
         pv[k].v[0] = mkd(l, __builtin_amdgcn_bitop3_b32(h, hi32(x[k]), m, 0x78));   // h ^ (v2c_k & m)
+        sink(k, pv[k]);
+        if constexpr (ORDER) {
+            __builtin_amdgcn_sched_group_barrier(0x2, LDPC_FAST64_STORE_VALU, 0);   // VALU: compare, selects, sign merge, address
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);   // DS write: this edge's store
+        }
     }
     return ok;
 }

@@ -10,6 +10,11 @@ namespace ldpc {
 
 enum { V_MS = 0, V_NMS = 1, V_OMS = 2 };
 
+// 1: fp32 pairs added as one packed v_pk_add_f32 (the round-1..3 code), 0: two v_add_f32.
+#ifndef LDPC_PK_ADD
+#define LDPC_PK_ADD 0
+#endif
+
 template <typename F> struct RowState;
 template <> struct __attribute__((aligned(16))) RowState<float> { float m1, m2; uint64_t meta; };
 template <> struct __attribute__((aligned(16))) RowState<double> { double m1, m2; uint64_t meta, pad; };
@@ -72,7 +77,26 @@ __device__ __forceinline__ int u16_at(const uint32_t (&w)[DC / 2], int k)
 // (ds_read_b64 / ds_write_b64 for two fp32 codewords or one fp64).
 template <typename F, int C> struct __attribute__((aligned(sizeof(F) * C))) Pack { F v[C]; };
 
-// s += r for every codeword of a pack (one v_pk_add_f32 for two fp32 codewords).
+// Plain IEEE fp32 add / subtract as one v_add_f32 / v_sub_f32 each. On gfx950 the
+// packed v_pk_add_f32 that -O3's SLP vectoriser forms from two adjacent adds issues
+// far slower than the two plain adds (MI355X_MICROARCH constants table; the fp32
+// ping-pong bit role measured 2 971 vs 2 097 cycles per interval for fp64's
+// v_add_f64 at the same instruction count), so the two codewords of an fp32 pair
+// are added separately. Same rounding (RNE), same values.
+__device__ __forceinline__ float fadd32(float a, float b)
+{
+    float r;
+    asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float fsub32(float a, float b)
+{
+    float r;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// s += r for every codeword of a pack.
 template <typename F, int C>
 __device__ __forceinline__ void padd(Pack<F, C> &s, const Pack<F, C> &r)
 {
@@ -82,12 +106,17 @@ __device__ __forceinline__ void padd(Pack<F, C> &s, const Pack<F, C> &r)
 template <>
 __device__ __forceinline__ void padd<float, 2>(Pack<float, 2> &s, const Pack<float, 2> &r)
 {
+#if LDPC_PK_ADD
     using V = float __attribute__((ext_vector_type(2)));
     V a, b;
     __builtin_memcpy(&a, &s, sizeof(V));
     __builtin_memcpy(&b, &r, sizeof(V));
     a += b;
     __builtin_memcpy(&s, &a, sizeof(V));
+#else
+    s.v[0] = fadd32(s.v[0], r.v[0]);
+    s.v[1] = fadd32(s.v[1], r.v[1]);
+#endif
 }
 
 // Bit nodes, edges k in [k, kend) of the first NACT slots (every one of them has
@@ -191,14 +220,19 @@ __device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DCA], Pack<f
 {
     static_assert(DC >= 1 && DC <= DCA, "cn_fast degree");
     constexpr uint32_t SIGN = 0x80000000u;
-    using V = float __attribute__((ext_vector_type(C)));   // C = 2: one v_pk_add_f32 per edge
+    using V = float __attribute__((ext_vector_type(C)));
     V x[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
+#if LDPC_PK_ADD
         V xi, pi;
         __builtin_memcpy(&xi, &xin[k], sizeof(V));
         __builtin_memcpy(&pi, &pv[k], sizeof(V));
         x[k] = xi - pi;                                                         // v2c (:469)
+#else
+#pragma unroll
+        for (int c = 0; c < C; ++c) x[k][c] = fsub32(xin[k].v[c], pv[k].v[c]);   // v2c (:469), one v_sub_f32 each
+#endif
     }
     bool ok = true;
 #pragma unroll

@@ -76,6 +76,12 @@ namespace {
 #ifndef LDPC_PP_PREFETCH
 #define LDPC_PP_PREFETCH 1
 #endif
+// 1: the fp64 check node's scatters are pinned in per-edge order behind each message's
+// selects (sched_group_barrier); 0: the machine scheduler places them (it tended to sink
+// all of a row's stores behind all of its selects, a 3 % swing between builds).
+#ifndef LDPC_PP_STORE_ORDER
+#define LDPC_PP_STORE_ORDER 1
+#endif
 
 // Diagnostic builds (-DLDPC_STAMPS, `make ppvariant`): per wave, s_memtime cycles
 // spent working and waiting at the interval barriers, to a.stamps[(block*16+wave)*2].
@@ -252,12 +258,21 @@ __device__ __forceinline__ void pp_account(const DecodeArgs &a, int *red, int gr
 
 // The check node of one row: fp64 (fast64.h cn_fast64) or an fp32 pair (cn_fast,
 // MS and NMS with the device-verified reciprocal; VAR picks).
-template <typename F, int DC, int VAR, bool FDIV, int C, int DCA>
+// store(k, message) scatters the new message of edge k: fp64 calls it as each message
+// is formed, in per-edge order (LDPC_PP_STORE_ORDER), so the scatters overlap the
+// selects of the later edges; fp32 after the row.
+template <typename F, int DC, int VAR, bool FDIV, int C, int DCA, typename Store>
 __device__ __forceinline__ bool pp_check_node(const Pack<F, C> (&xin)[DCA], Pack<F, C> (&pv)[DCA], F alpha, F rcp,
-                                              F delta)
+                                              F delta, Store store)
 {
-    if constexpr (sizeof(F) == 8) return cn_fast64<DC, VAR, FDIV>(xin, pv, alpha, rcp, delta);
-    else return cn_fast<DC, C>(xin, pv, VAR == V_NMS, alpha, rcp);
+    if constexpr (sizeof(F) == 8) {
+        return cn_fast64<DC, VAR, FDIV, DCA, Store, LDPC_PP_STORE_ORDER != 0>(xin, pv, alpha, rcp, delta, store);
+    } else {
+        const bool ok = cn_fast<DC, C>(xin, pv, VAR == V_NMS, alpha, rcp);
+#pragma unroll
+        for (int k = 0; k < DC; ++k) store(k, pv[k]);
+        return ok;
+    }
 }
 
 // ---- one wave's work: R check rows of each slot, or (HB) CPT bit slots ----
@@ -422,23 +437,25 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                             for (int k = 0; k < DCr; ++k) xin[r][k] = lds_at<P>(addr8<DCX>(colw[r], k, ab));
                         }
                         bool ok = true;
-                        if constexpr (LDPC_PP_EXP == 3) {
-#pragma unroll
-                            for (int k = 0; k < DCr; ++k)
-#pragma unroll
-                                for (int c = 0; c < C; ++c) prev[X][r][k].v[c] = xin[r][k].v[c] - prev[X][r][k].v[c];
-                        } else {
-                            ok = pp_check_node<F, DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta);
-                        }
-                        if (!ok && deg[r] > 0 && LDPC_PP_EXP == 0) s.red[X] = 1;   // experiments: never re-decode
-                        if constexpr (LDPC_PP_EXP != 4) {
-#pragma unroll
-                            for (int k = 0; k < DCr; ++k)
+                        // the scatter of edge k into the bit-slot layout (experiments: none, or lane-contiguous)
+                        auto store = [&](int k, const P &m) {
+                            if constexpr (LDPC_PP_EXP != 4)
                                 lds_put<P>((LDPC_PP_EXP == 6 || LDPC_PP_EXP == 7)
                                                ? cb + 8u * (uint32_t)(lane + 64 * ((k + 8 * r + 16 * (tid >> 6)) % 112))
                                                : addr8<DCX>(posw[r], k, cb),
-                                           prev[X][r][k]);
+                                           m);
+                        };
+                        if constexpr (LDPC_PP_EXP == 3) {
+#pragma unroll
+                            for (int k = 0; k < DCr; ++k) {
+#pragma unroll
+                                for (int c = 0; c < C; ++c) prev[X][r][k].v[c] = xin[r][k].v[c] - prev[X][r][k].v[c];
+                                store(k, prev[X][r][k]);
+                            }
+                        } else {
+                            ok = pp_check_node<F, DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta, store);
                         }
+                        if (!ok && deg[r] > 0 && LDPC_PP_EXP == 0) s.red[X] = 1;   // experiments: never re-decode
                         if (R > 1 && LDPC_PP_ROWFENCE) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
                     });
                 }

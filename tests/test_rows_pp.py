@@ -170,3 +170,60 @@ def test_pp_row_slot_layouts_equal_each_other_and_oracle(tmp_path, monkeypatch, 
     y, d = outs["split"][0], outs["split"][1]
     want = O.Alist(path).decode(y[:64], 30, O.Cfg(variant=1, alpha=1.25), workers=16)
     assert int((d[:64] != want).sum()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch,T,v", [
+    (2048, 50, dict(variant=1, alpha=1.25)),     # the bench configuration
+    (1003, 50, dict(variant=0)),                 # batch 1003 = 250 steps of 4 + 3: the last step's partner missing
+    (2, 7, dict(variant=1, alpha=1.25)),         # one pair, the other slot empty
+    (5, 0, dict(variant=0)),                     # no iteration
+])
+def test_pp_fp32_pairs_equal_row_kernel_and_oracle(gpu_ctx_factory, monkeypatch, batch, T, v):
+    """fp32 pairs on the ping-pong kernel (LDPC_ROWS32=pp: two float2 slots, four codewords
+    per block step) give the fp32 row kernel's channel, decisions, per-frame results and
+    counters, and the fp32 oracle's decisions (decodeMinSum.cpp:410-476 in float)."""
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(CODE)
+    cfg = native.DecoderConfig(T=T, precision=native.F32, **v)
+    monkeypatch.delenv("LDPC_ROWS32", raising=False)
+    assert ctx.kernel_info(cfg)["kernel"] == "rows"
+    y0, d0, f0, c0 = ctx.sim_trace(1.5, 0.5, cfg, seed=78, stream_id=6, first_cw=321, batch=batch)
+    monkeypatch.setenv("LDPC_ROWS32", "pp")
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
+    y1, d1, f1, c1 = ctx.sim_trace(1.5, 0.5, cfg, seed=78, stream_id=6, first_cw=321, batch=batch)
+    assert ctx.redo_count() == 0
+    assert np.array_equal(y0, y1) and np.array_equal(d0, d1) and np.array_equal(f0, f1)
+    assert c0.as_dict() == c1.as_dict()
+    n = min(batch, 128)
+    want = O.Alist(code_path(CODE)).decode(y1[:n], T, O.Cfg(**v), workers=16)
+    assert int((d1[:n] != want).sum()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0))])
+def test_pp_fp32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, vname, v):
+    """fp32 pairs: frames whose inputs or messages leave the fast premise (|y| >= 1e30,
+    inf, NaN, growth past 1e30) hand their pair to the exact re-decode; every decision
+    equals the fp32 oracle's and the other pair of the step is unaffected."""
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(CODE)
+    monkeypatch.setenv("LDPC_ROWS32", "pp")
+    N = ctx.graph.N
+    y = _glibc_frames(N, 12, 1.5, 0.5, seed=4245).astype(np.float32)
+    y[1] *= np.float32(1e31)
+    y[3, 5] = np.inf
+    y[4, 7] = np.nan
+    y[6, ::3] = -0.0
+    y[9] *= np.float32(1e28)
+    A = O.Alist(code_path(CODE))
+    for T in (1, 7, 30):
+        cfg = native.DecoderConfig(T=T, precision=native.F32, **v)
+        assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
+        d, fr, cnt = ctx.decode(y, cfg)
+        want = A.decode(y, T, O.Cfg(**v), workers=8)
+        mism = (d != want).sum(axis=1)
+        assert int(mism.sum()) == 0, f"T={T}: mismatching frames {np.nonzero(mism)[0].tolist()}"
+        assert np.array_equal(fr["bit_err"], (want != 1).sum(axis=1))
+        assert cnt.frames == len(y) and cnt.iters == T * len(y)
+        assert ctx.redo_count() >= 4        # the pairs of frames 1, 3, 4 (and 9 once it grows)
