@@ -339,6 +339,26 @@ def lds_model(si: dict, N: int) -> dict:
     return {"cycles_per_group_iter": sum(cyc.values()), "by_phase": cyc, "cw_per_group": si["cw_per_block"]}
 
 
+def lds_models_alt(si: dict, deg, N: int, kernel: str) -> dict:
+    """Two companions of lds_model's padded row-schedule model (the one `frac` uses, as
+    in rounds 2-3): `issued` -- the wave-instructions the kernel actually issues (the
+    ping-pong kernel's degree-aware slots, graph.h pp_row_slots: 7-edge check nodes in
+    768 of the 1024 row slots when every row of degree > 7 fits the other 256), and
+    `edges` -- the algorithmic minimum, E gathers + E scatters + E bit reads + N app
+    writes in 64-lane wave-instructions, no padding."""
+    deg = np.asarray(deg, dtype=np.int64)
+    rows = si["threads"] * si["rows_per_thread"]
+    split = (kernel == "rows_pp" and si["dc"] == 8 and si["rows_per_thread"] == 2 and si["threads"] == 512
+             and os.environ.get("LDPC_PP_ROWS", "") != "plain" and int((deg > 7).sum()) <= 256 and len(deg) <= rows)
+    slot_edges = (768 * 7 + 256 * 8) if split else rows * si["dc"]
+    rd, wr = LDS_CYC["ds_read_b64"], LDS_CYC["ds_write_b64"]
+    issued = slot_edges / 64 * (rd + wr) + si["e_pad"] / 64 * rd + si["threads"] * si["slots_per_thread"] / 64 * wr
+    E = int(deg.sum())
+    edges = E / 64 * (rd + wr + rd) + N / 64 * wr
+    return {"issued": {"cycles_per_group_iter": issued, "degree_split": bool(split)},
+            "edges": {"cycles_per_group_iter": edges, "E": E}}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -373,6 +393,7 @@ def main():
     from ldpcsimulation_amd import codes, native
     alist = codes.ensure_80211n_1944()
     g = native.Graph.from_alist(alist)
+    row_deg = [len(r) for r in codes.read_alist(alist).rows]
     B = args.batch
     ctx = native.Context(g, local if world > 1 else 0, B)
     # A dedicated (non-default) torch stream: the library launches on it, so the
@@ -451,9 +472,12 @@ def main():
         n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
         achieved = cycles / avg_kernel_s / 1e9
         peak = n_cu * CLOCK_HZ / 1e9
+        alt = lds_models_alt(si, row_deg, g.N, info["kernel"])
+        for k, v in alt.items():
+            v["frac"] = v["cycles_per_group_iter"] * args.T * groups / avg_kernel_s / 1e9 / peak
         out.update({"bound": "lds", "achieved": achieved, "peak": peak, "unit": "G LDS-cycles/s",
                     "frac": achieved / peak, "lds_cycles_per_launch": cycles, "cus": n_cu,
-                    "lds_model": m, "row_sched": si})
+                    "lds_model": m, "lds_model_alt": alt, "row_sched": si})
         return out
 
     if rank == 0:

@@ -58,6 +58,25 @@ static void one_code(const char *path)
                         CHECK((int)rs.cn_cols.size() == threads * rpt * dc, "%s: row schedule size", path);
                     }
                 }
+    // the ping-pong kernel's degree-aware row slots: a permutation of the rows in which
+    // every capped slot (row 0 of every thread, row 1 of the upper half) holds degree <= 7
+    for (int threads : {128, 512}) {
+        const std::vector<int> slots = ldpc::pp_row_slots(g, threads, 7);
+        if (slots.empty()) continue;
+        std::vector<int> seen(g.M, 0);
+        for (size_t t = 0; t < slots.size(); ++t) {
+            const int j = slots[t];
+            if (j < 0) continue;
+            CHECK(j < g.M && !seen[j]++, "%s: pp_row_slots not a permutation", path);
+            const bool capped = t < (size_t)threads || (int)(t % threads) >= threads / 2;
+            CHECK(!capped || g.row_deg[j] <= 7, "%s: degree-%d row in a capped slot", path, (int)g.row_deg[j]);
+        }
+        for (int j = 0; j < g.M; ++j) CHECK(seen[j] == 1, "%s: row %d missing from pp_row_slots", path, j);
+        ldpc::RowSchedule rs;
+        const std::string er = ldpc::build_row_schedule(g, threads, 4, 8, 2, rs, &slots);
+        CHECK(er.empty() || er == "bits exceed slots", "%s: pp row schedule (%s)", path, er.c_str());
+        ++rows;
+    }
     ldpc::FloodSchedule fs;
     const std::string ef = ldpc::build_flood_schedule(g, fs);
     if (ef.empty()) {
