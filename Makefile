@@ -36,18 +36,24 @@ ALIGNFLAGS = -falign-loops=32
 # bench launch over 3 interleaved rounds, stable under code shifts;
 # `make ppvariant PPSCHED= VFLAGS="-mllvm -amdgpu-sched-strategy=..."` for others.
 PPSCHED ?= -mllvm -amdgpu-sched-strategy=max-memory-clause
+# No SLP vectorisation where the compiler would pair scalar fp32 adds into v_pk_add_f32,
+# which issues slower on gfx950 than the two plain adds it replaces (measured: EMS
+# 7.85-7.95 -> 8.38-8.50 Gbit/s at 2.0 dB, fp32 layered DVB-S2 44.6 -> 42.2 ms, GDBF
+# rows 21.7 -> 21.3 ms; flooding and BP equal). Explicit vector types (the fp32 row
+# kernel's pairs) are not affected.
+NOSLP = -fno-slp-vectorize
 $(LIBDIR)/obj/kernels.o: $(CSRC)/kernels.hip $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(NOSLP) -c -o $@ $<
 $(LIBDIR)/obj/rows_fast.o: $(CSRC)/rows_fast.hip $(CSRC)/fast64.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/rows_pp.o: $(CSRC)/rows_pp.hip $(CSRC)/fast64.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) -c -o $@ $<
 $(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(NOSLP) -c -o $@ $<
 $(LIBDIR)/obj/bp.o: $(CSRC)/bp.hip $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/nb.o: $(CSRC)/nb.hip $(CSRC)/nb.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(NOSLP) -c -o $@ $<
 $(LIBDIR)/obj/nb_api.o: $(CSRC)/nb_api.cpp $(CSRC)/nb.h $(CSRC)/kernels.h include/ldpc_hip.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/api.o: $(CSRC)/api.cpp $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/gdbf.h $(CSRC)/graph.h include/ldpc_hip.h | $(LIBDIR)/obj
@@ -97,7 +103,7 @@ $(BINDIR)/decodeStochasticNGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BIN
 # Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> lib/variants/libldpc_hip_x.so
 variant:
 	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(NOSLP) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/api.o $(CSRC)/api.cpp
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/graph.o
@@ -120,14 +126,14 @@ ppvariant: $(OBJS)
 NBSRC ?= $(CSRC)/nb.hip
 nbvariant: $(OBJS)
 	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/nb.o $(NBSRC)
+	$(HIPCC) $(HIPFLAGS) $(NOSLP) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/nb.o $(NBSRC)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/nb.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/nb.o
 
 # GDBF kernel A/B variants: make gdbfvariant NAME=x VFLAGS="-DLDPC_GDBF_..." -> lib/variants/libldpc_hip_x.so
 gdbfvariant: $(OBJS)
 	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/gdbf.o $(CSRC)/gdbf.hip
+	$(HIPCC) $(HIPFLAGS) $(NOSLP) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/gdbf.o $(CSRC)/gdbf.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/gdbf.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/gdbf.o
 

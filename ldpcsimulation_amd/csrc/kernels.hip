@@ -21,6 +21,12 @@
 // no FMA may fuse the channel's 1 + sigma*n or the quantiser.
 #include "kernels.h"
 #include "device_common.h"
+// The fp32 row kernel (k_decode_rows) adds its pairs as one v_pk_add_f32: two plain
+// v_add_f32 measured 10.0 vs 8.8 ms per bench launch there (the ping-pong kernel is the
+// other way round: minsum_common.h).
+#ifndef LDPC_PK_ADD
+#define LDPC_PK_ADD 1
+#endif
 #include "minsum_common.h"
 
 #include <hip/hip_runtime.h>

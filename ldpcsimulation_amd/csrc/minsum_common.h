@@ -304,4 +304,99 @@ __device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DCA], Pack<f
     return ok;
 }
 
+// cn_fast for an fp32 pair (C = 2) with the outputs produced edge by edge: both
+// codewords' minima, parity and normalised magnitudes first, then for each edge k
+// the two compares and selects and sink(k, message) -- with ORDER the scheduler is
+// asked to keep that per-edge order (the ping-pong kernel's scatters then overlap
+// the later edges' selects, as cn_fast64's do). Same values as cn_fast<DC, 2>.
+struct NoSink32 {
+    __device__ __forceinline__ void operator()(int, const Pack<float, 2> &) const {}
+};
+#ifndef LDPC_FAST32_STORE_VALU
+#define LDPC_FAST32_STORE_VALU 4
+#endif
+template <int DC, int DCA = DC, typename Sink = NoSink32, bool ORDER = false>
+__device__ __forceinline__ bool cn_fast_pair(const Pack<float, 2> (&xin)[DCA], Pack<float, 2> (&pv)[DCA], bool nms,
+                                             float alpha, float rcp, Sink sink = Sink())
+{
+    static_assert(DC >= 1 && DC <= DCA, "cn_fast_pair degree");
+    constexpr uint32_t SIGN = 0x80000000u;
+    float x[2][DC];
+#pragma unroll
+    for (int k = 0; k < DC; ++k)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) x[c][k] = fsub32(xin[k].v[c], pv[k].v[c]);   // v2c (:469)
+    bool ok = true;
+    float mn1[2], s1f[2], s2f[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        constexpr int G = (DC + 2) / 3;
+        float lo[G], sec[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int k0 = 3 * g, n = DC - k0 < 3 ? DC - k0 : 3;
+            const float a0 = __builtin_fabsf(x[c][k0]);
+            if (n == 3) {
+                const float a1 = __builtin_fabsf(x[c][k0 + 1]), a2 = __builtin_fabsf(x[c][k0 + 2]);
+                lo[g] = __builtin_fminf(__builtin_fminf(a0, a1), a2);
+                sec[g] = __builtin_amdgcn_fmed3f(a0, a1, a2);
+            } else if (n == 2) {
+                const float a1 = __builtin_fabsf(x[c][k0 + 1]);
+                lo[g] = __builtin_fminf(a0, a1);
+                sec[g] = __builtin_fmaxf(a0, a1);
+            } else {
+                lo[g] = a0;
+                sec[g] = __builtin_huge_valf();
+            }
+        }
+        float m1, m2;
+        if constexpr (G == 3) {
+            m1 = __builtin_fminf(__builtin_fminf(lo[0], lo[1]), lo[2]);
+            m2 = __builtin_fminf(__builtin_amdgcn_fmed3f(lo[0], lo[1], lo[2]),
+                                 __builtin_fminf(__builtin_fminf(sec[0], sec[1]), sec[2]));
+        } else {
+            m1 = lo[0];
+            m2 = sec[0];
+#pragma unroll
+            for (int g = 1; g < G; ++g) {
+                m2 = __builtin_amdgcn_fmed3f(m1, lo[g], __builtin_fminf(m2, sec[g]));
+                m1 = __builtin_fminf(m1, lo[g]);
+            }
+        }
+        uint32_t par = 0;
+#pragma unroll
+        for (int k = 0; k + 1 < DC; k += 2)
+            par = __builtin_amdgcn_bitop3_b32(par, __float_as_uint(x[c][k]), __float_as_uint(x[c][k + 1]), 0x96);
+        if (DC & 1) par ^= __float_as_uint(x[c][DC - 1]);
+        float M1 = m1, M2 = m2;
+        if (nms) {   // x/alpha = q + (x - q*alpha)*r, q = x*r (verified for all finite x); inf/alpha = inf
+            const float q1 = m1 * rcp, q2 = m2 * rcp;
+            const float d1 = __builtin_fmaf(__builtin_fmaf(-q1, alpha, m1), rcp, q1);
+            const float d2 = __builtin_fmaf(__builtin_fmaf(-q2, alpha, m2), rcp, q2);
+            M1 = m1 < __builtin_huge_valf() ? d1 : m1;
+            M2 = m2 < __builtin_huge_valf() ? d2 : m2;
+        }
+        ok &= M2 < 1e30f;
+        uint32_t a1 = __float_as_uint(M1) ^ (par & SIGN), a2 = __float_as_uint(M2) ^ (par & SIGN);
+        asm("" : "+v"(a1), "+v"(a2));   // keep the parity out of the per-edge select
+        mn1[c] = m1;
+        s1f[c] = __uint_as_float(a1);
+        s2f[c] = __uint_as_float(a2);
+    }
+#pragma unroll
+    for (int k = 0; k < DC; ++k) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t m = (__builtin_fabsf(x[c][k]) == mn1[c]) ? __float_as_uint(s2f[c]) : __float_as_uint(s1f[c]);
+            pv[k].v[c] = __uint_as_float(__builtin_amdgcn_bitop3_b32(m, __float_as_uint(x[c][k]), SIGN, 0x78));
+        }
+        sink(k, pv[k]);
+        if constexpr (ORDER) {
+            __builtin_amdgcn_sched_group_barrier(0x2, LDPC_FAST32_STORE_VALU, 0);   // 2 compares, 2 selects, 2 merges, address
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+    }
+    return ok;
+}
+
 }  // namespace ldpc

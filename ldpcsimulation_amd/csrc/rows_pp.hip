@@ -82,6 +82,11 @@ namespace {
 #ifndef LDPC_PP_STORE_ORDER
 #define LDPC_PP_STORE_ORDER 1
 #endif
+// 1: the scheduler is asked to issue all of an interval's gathers before the check-node
+// arithmetic (sched_group_barrier); 0: left to the scheduler.
+#ifndef LDPC_PP_GATHER_FIRST
+#define LDPC_PP_GATHER_FIRST 0
+#endif
 
 // Diagnostic builds (-DLDPC_STAMPS, `make ppvariant`): per wave, s_memtime cycles
 // spent working and waiting at the interval barriers, to a.stamps[(block*16+wave)*2].
@@ -258,9 +263,9 @@ __device__ __forceinline__ void pp_account(const DecodeArgs &a, int *red, int gr
 
 // The check node of one row: fp64 (fast64.h cn_fast64) or an fp32 pair (cn_fast,
 // MS and NMS with the device-verified reciprocal; VAR picks).
-// store(k, message) scatters the new message of edge k: fp64 calls it as each message
-// is formed, in per-edge order (LDPC_PP_STORE_ORDER), so the scatters overlap the
-// selects of the later edges; fp32 after the row.
+// store(k, message) scatters the new message of edge k, called as each message is
+// formed, in per-edge order (LDPC_PP_STORE_ORDER), so the scatters overlap the selects
+// of the later edges (fp64: cn_fast64; fp32 pairs: cn_fast_pair).
 template <typename F, int DC, int VAR, bool FDIV, int C, int DCA, typename Store>
 __device__ __forceinline__ bool pp_check_node(const Pack<F, C> (&xin)[DCA], Pack<F, C> (&pv)[DCA], F alpha, F rcp,
                                               F delta, Store store)
@@ -268,10 +273,7 @@ __device__ __forceinline__ bool pp_check_node(const Pack<F, C> (&xin)[DCA], Pack
     if constexpr (sizeof(F) == 8) {
         return cn_fast64<DC, VAR, FDIV, DCA, Store, LDPC_PP_STORE_ORDER != 0>(xin, pv, alpha, rcp, delta, store);
     } else {
-        const bool ok = cn_fast<DC, C>(xin, pv, VAR == V_NMS, alpha, rcp);
-#pragma unroll
-        for (int k = 0; k < DC; ++k) store(k, pv[k]);
-        return ok;
+        return cn_fast_pair<DC, DCA, Store, LDPC_PP_STORE_ORDER != 0>(xin, pv, VAR == V_NMS, alpha, rcp, store);
     }
 }
 
@@ -410,6 +412,12 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                             xin[r][k] = lds_at<P>((LDPC_PP_EXP == 5 || LDPC_PP_EXP == 7) ? ab + 8u * (uint32_t)(lane + 64 * (k + 8 * r))
                                                                                          : addr8<DCX>(colw[r], k, ab));
                     });
+                    if constexpr (LDPC_PP_GATHER_FIRST && LDPC_PP_PREFETCH) {
+                        // every gather of the interval issued ahead of the check-node arithmetic
+                        constexpr int NG = DC0 + (R > 1 ? DC1 : 0);
+                        __builtin_amdgcn_sched_group_barrier(0x2, NG, 1);     // their addresses
+                        __builtin_amdgcn_sched_group_barrier(0x100, NG, 1);   // the ds_read_b64s
+                    }
                 }
             }
             if constexpr (HB) {
