@@ -558,9 +558,11 @@ static const ldpc::RowSched &pp_sched(const ldpc_ctx *c)
 //         check and bit waves overlapped) when the schedule fits it, else the
 //         one-codeword-per-block k_rows_fast (LDPC_ROWS=fast forces the latter);
 //   fp32: pairs as float2 -- MS and NMS with the verified reciprocal (a after
-//         nms_setup) -- on the ping-pong kernel with LDPC_ROWS32=pp, on the pair
-//         instance of k_rows_fast with LDPC_ROWS32=fast; otherwise the row kernel
-//         (kernels.hip k_decode_rows, fast and exact loops in one).
+//         nms_setup) -- on the ping-pong kernel (7.4 vs 8.8 ms per bench launch for
+//         the row kernel), on the pair instance of k_rows_fast with
+//         LDPC_ROWS32=fast, on the row kernel (kernels.hip k_decode_rows, fast and
+//         exact loops in one) with LDPC_ROWS32=rows and for everything else (OMS,
+//         codes the ping-pong schedule does not fit).
 // LDPC_ROWS=old keeps the row kernel for both.
 enum class FastKind { none, pp, fast };
 static FastKind fast_kind(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
@@ -577,8 +579,8 @@ static FastKind fast_kind(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool 
     const char *e32 = std::getenv("LDPC_ROWS32");
     if (e32 && std::strcmp(e32, "fast") == 0)
         return ldpc::rows_fast_supported(c->rs, false) ? FastKind::fast : FastKind::none;
-    if (e32 && std::strcmp(e32, "pp") == 0) return pp_ok ? FastKind::pp : FastKind::none;
-    return FastKind::none;
+    if (e32 && std::strcmp(e32, "rows") == 0) return FastKind::none;
+    return pp_ok ? FastKind::pp : FastKind::none;
 }
 static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
 {

@@ -181,8 +181,11 @@ def test_all_kernels_bit_identical(monkeypatch, code):
         if code != "4000.2000.4.244.alist":
             # fp64: the ping-pong kernel (rows_pp.hip, M in 513..1024) or the one-codeword
             # fast-path kernel (rows_fast.hip); fp32: the row kernel
-            f64_default = "rows_pp" if code == "80211n_1944_r12.alist" else "rows_fast"
-            assert names["default"] == (f64_default if prec == native.F64 else "rows")
+            pp_code = code == "80211n_1944_r12.alist"
+            f64_default = "rows_pp" if pp_code else "rows_fast"
+            # fp32: pairs on the ping-pong kernel for MS / verified-reciprocal NMS, else the row kernel
+            f32_default = "rows_pp" if pp_code and cfg.variant != native.OMS else "rows"
+            assert names["default"] == (f64_default if prec == native.F64 else f32_default)
         outs = {k: c.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300) for k, c in ctxs.items()}
         monkeypatch.setenv("LDPC_ROWS", "fast")   # fp64: the one-codeword fast kernel where pp is the default
         outs["rows_fast"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
@@ -192,6 +195,8 @@ def test_all_kernels_bit_identical(monkeypatch, code):
         monkeypatch.delenv("LDPC_ROWS", raising=False)
         monkeypatch.setenv("LDPC_ROWS32", "fast")   # fp32: the pair instance of rows_fast (opt-in)
         outs["rows_fast32"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
+        monkeypatch.setenv("LDPC_ROWS32", "rows")   # fp32: the row kernel
+        outs["rows32"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
         monkeypatch.delenv("LDPC_ROWS32", raising=False)
         ref = outs["global"]
         for k, o in outs.items():

@@ -90,7 +90,9 @@ def test_fast_kernel_is_the_f64_row_kernel(gpu_ctx_factory, monkeypatch, code):
     assert ctx.kernel_info(cfg)["kernel"] == ("rows_pp" if code == "80211n_1944_r12.alist" else "rows_fast")
     monkeypatch.setenv("LDPC_ROWS", "fast")
     assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
-    cfg.precision = native.F32                       # fp32: the row kernel by default
+    cfg.precision = native.F32                       # fp32: pairs on the ping-pong kernel where it fits
+    assert ctx.kernel_info(cfg)["kernel"] == ("rows_pp" if code == "80211n_1944_r12.alist" else "rows")
+    monkeypatch.setenv("LDPC_ROWS32", "rows")
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
 
 
@@ -179,7 +181,7 @@ def test_f32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, 
         assert cnt.frames == len(y) and cnt.bit_err == int(w.sum()) and cnt.iters == T * len(y)
         # pairs (0,1), (2,3), (4,5) break (frame 5 shares frame 4's pair); a pair is re-decoded whole
         assert redo == 6, redo
-        monkeypatch.delenv("LDPC_ROWS32")
+        monkeypatch.setenv("LDPC_ROWS32", "rows")
         assert ctx.kernel_info(cfg)["kernel"] == "rows"
         d_old, fr_old, cnt_old = ctx.decode(y, cfg)
         monkeypatch.setenv("LDPC_ROWS32", "fast")
@@ -215,18 +217,22 @@ def test_f64_headline_config_bit_exact(gpu_ctx_factory, monkeypatch, kernel, ebn
 def test_f32_bench_kernel_bit_exact_at_T50(gpu_ctx_factory, monkeypatch, ebn0, vname, v):
     """The fp32 bench kernel (k_decode_rows<float, PHILOX, 2, 8, 4, 2>: fast check node,
     reciprocal NMS, fast->exact hand-over) at the bench's T=50 on 2048 codewords per
-    point: decisions identical to the fp32 oracle on the same y, and
-    to the opt-in pair instance of rows_fast (LDPC_ROWS32=fast)."""
+    point: decisions identical to the fp32 oracle on the same y, to
+    the opt-in pair instance of rows_fast (LDPC_ROWS32=fast) and to the fp32 default,
+    the ping-pong kernel's float2 slots (rows_pp.hip)."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory("80211n_1944_r12.alist")
     cfg = native.DecoderConfig(T=50, precision=native.F32, **v)
+    monkeypatch.setenv("LDPC_ROWS32", "rows")
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
     y, d, fr, cnt = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261017, stream_id=2, first_cw=0, batch=2048)
-    monkeypatch.setenv("LDPC_ROWS32", "fast")
-    y_f, d_f, fr_f, _ = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261017, stream_id=2, first_cw=0, batch=2048)
-    assert ctx.redo_count() == 0
+    for k32, name in (("fast", "rows_fast"), ("pp", "rows_pp")):   # the opt-in pair kernel, the fp32 default
+        monkeypatch.setenv("LDPC_ROWS32", k32)
+        assert ctx.kernel_info(cfg)["kernel"] == name
+        y_f, d_f, fr_f, _ = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261017, stream_id=2, first_cw=0, batch=2048)
+        assert ctx.redo_count() == 0
+        assert np.array_equal(y_f, y) and np.array_equal(d_f, d) and np.array_equal(fr_f, fr), k32
     monkeypatch.delenv("LDPC_ROWS32")
-    assert np.array_equal(y_f, y) and np.array_equal(d_f, d) and np.array_equal(fr_f, fr)
     want = O.Alist(code_path("80211n_1944_r12.alist")).decode(y, 50, O.Cfg(**v), workers=16)
     assert int((d != want).sum()) == 0
     assert np.array_equal(fr["bit_err"], (want != 1).sum(axis=1))

@@ -180,16 +180,16 @@ def test_pp_row_slot_layouts_equal_each_other_and_oracle(tmp_path, monkeypatch, 
     (5, 0, dict(variant=0)),                     # no iteration
 ])
 def test_pp_fp32_pairs_equal_row_kernel_and_oracle(gpu_ctx_factory, monkeypatch, batch, T, v):
-    """fp32 pairs on the ping-pong kernel (LDPC_ROWS32=pp: two float2 slots, four codewords
+    """fp32 pairs on the ping-pong kernel (the fp32 default: two float2 slots, four codewords
     per block step) give the fp32 row kernel's channel, decisions, per-frame results and
     counters, and the fp32 oracle's decisions (decodeMinSum.cpp:410-476 in float)."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(CODE)
     cfg = native.DecoderConfig(T=T, precision=native.F32, **v)
-    monkeypatch.delenv("LDPC_ROWS32", raising=False)
+    monkeypatch.setenv("LDPC_ROWS32", "rows")
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
     y0, d0, f0, c0 = ctx.sim_trace(1.5, 0.5, cfg, seed=78, stream_id=6, first_cw=321, batch=batch)
-    monkeypatch.setenv("LDPC_ROWS32", "pp")
+    monkeypatch.delenv("LDPC_ROWS32")                 # the fp32 default
     assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
     y1, d1, f1, c1 = ctx.sim_trace(1.5, 0.5, cfg, seed=78, stream_id=6, first_cw=321, batch=batch)
     assert ctx.redo_count() == 0
