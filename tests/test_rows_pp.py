@@ -115,19 +115,23 @@ def test_pp_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, v
 
 
 def _random_code(tmp_path, name, N, M, row_deg, seed):
-    """A random code with the given row degrees (a list, one per row); every bit in >= 1 check."""
+    """A random code with the given row degrees (a list, one per row, sum >= N) in which
+    every bit is in at least one check: the first N edge slots take a permutation of the
+    bits, the rest random bits (redrawn on a duplicate within the row)."""
     from ldpcsimulation_amd import codes
     rng = np.random.default_rng(seed)
-    rows = []
+    assert sum(row_deg) >= N
+    pool = list(rng.permutation(N)) + list(rng.integers(0, N, size=sum(row_deg) - N))
+    rows, at = [], 0
     for j in range(M):
-        rows.append(sorted(rng.choice(N, size=row_deg[j], replace=False).tolist()))
-    seen = {v for r in rows for v in r}
-    for v in range(N):                      # cover bits no row picked (adds an edge to a short row)
-        if v not in seen:
-            j = int(rng.integers(M))
-            while v in rows[j] or len(rows[j]) >= max(row_deg):
-                j = int(rng.integers(M))
-            rows[j] = sorted(rows[j] + [v])
+        r = []
+        for _ in range(row_deg[j]):
+            v = int(pool[at])
+            at += 1
+            while v in r:
+                v = int(rng.integers(N))
+            r.append(v)
+        rows.append(sorted(r))
     path = str(tmp_path / name)
     codes.write_alist(codes.ParityCheck.from_rows(N, rows), path)
     return path
