@@ -183,7 +183,9 @@ def test_sweep_checkpoint_resume(tmp_path):
     """SURVEY §5 checkpoint/resume on the HIP path: `sweep.py --checkpoint` writes the
     uninterrupted run's log lines; with its .partial file cut back to mid-point
     states (a sweep killed during point 1), a restart resumes both points and appends
-    the same lines; a restart of a finished sweep decodes and appends nothing."""
+    the same lines; a restart of a finished sweep decodes and appends nothing. (The
+    default --checkpoint-interval of 10 s records at most one round per 10 s; this
+    test records every round.)"""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     args = [code_path(CODE), "--rate", "0.5", "--snr", "1.5", "1.75", "-T", "50", "--variant", "nms",
             "--alpha", "1.25", "--batch", "2048", "--seed", "777", "--json"]
@@ -197,7 +199,7 @@ def test_sweep_checkpoint_resume(tmp_path):
     run("--log", str(tmp_path / "full.txt"))
     want = (tmp_path / "full.txt").read_text().splitlines()
     ck = tmp_path / "ck.partial"
-    run("--log", str(tmp_path / "a.txt"), "--checkpoint", str(ck))
+    run("--log", str(tmp_path / "a.txt"), "--checkpoint", str(ck), "--checkpoint-interval", "0")   # every round
     assert (tmp_path / "a.txt").read_text().splitlines() == want
     recs = [json.loads(l) for l in ck.read_text().splitlines()]
     r1 = [r for r in recs if r["kind"] == "round" and r["k"] == 1]
