@@ -25,6 +25,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace ldpc {
@@ -40,6 +41,31 @@ constexpr float kInf = __builtin_huge_valf();
 #ifndef LDPC_EMS_EXP
 #define LDPC_EMS_EXP 0
 #endif
+// Diagnostic builds (-DLDPC_EMS_STAMPS, `make nbvariant`): per wave, s_memtime cycles
+// per phase summed over the block's codewords, appended to $LDPC_EMS_STAMPS by nb_launch
+// ([block][wave][8]: channel+init, check work, check wait, symbol work, symbol wait,
+// syndrome, accounting, codewords). Never in the shipped kernel.
+#ifdef LDPC_EMS_STAMPS
+constexpr int kEmsStampBlocks = 256;
+__device__ unsigned long long g_ems_stamps[kEmsStampBlocks * 16 * 8];
+struct EmsStamps {
+    unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t = 0;
+    __device__ void start() { t = __builtin_amdgcn_s_memtime(); }
+    __device__ void lap(int k)
+    {
+        const unsigned long long n = __builtin_amdgcn_s_memtime();
+        v[k] += n - t;
+        t = n;
+    }
+};
+#define EMS_LAP(k) st.lap(k)
+#else
+struct EmsStamps {
+    __device__ void start() {}
+};
+#define EMS_LAP(k) ((void)0)
+#endif
 // Symbol nodes of degree <= LDPC_EMS_VD keep their c2v in registers (0: re-read).
 #ifndef LDPC_EMS_VD
 #define LDPC_EMS_VD 2
@@ -50,16 +76,20 @@ constexpr float kInf = __builtin_huge_valf();
 // Edge slots are position-major: slot(j, k) = k*M + j for check j and mlist
 // position k, so the check-node lanes of a wave (consecutive j, same k) read
 // consecutive 16-byte chunks. Messages are stored in the CHECK domain,
-// chunk-major: entry x of slot s at float ((x >> 2) * Ep + s) * 4 + (x & 3),
-// with Ep = slots rounded to 2 mod 8 (spreads the symbol-node gathers over
-// the banks).
+// chunk-major: entry x of slot s at float ((x >> 2) * Ep + (s ^ (x >> 2))) * 4 + (x & 3),
+// Ep = 2^k slots (nb_ep), i.e. byte (s << 4) ^ nb_lambda(x, k): XOR-linear in x, so the
+// symbol node's 16 gather addresses of an edge are one XOR each (Gray order). The
+// chunk index XOR-ed into the slot's low bits spreads those gathers over the banks;
+// a check wave's 16-byte chunks stay one permutation of consecutive units.
 struct NbSched {
-    int Ep, M;
+    int Ep, M, sh;           // sh = log2(Ep) + 4: the chunk bits of a byte offset
     const uint8_t *cn_d;     // [M]    check degree
     const uint32_t *vn;      // [N]    first col entry << 8 | degree
     const uint16_t *vslot;   // [E]    slots of each symbol, nlist order
     const uint8_t *vh;       // [E]    their coefficients
 };
+
+typedef __attribute__((address_space(3))) float LdsF;
 
 // GF(16) (x^4 + x + 1): v * x.
 __device__ __forceinline__ int gf16_xt(int v) { return ((v << 1) & 15) ^ ((v & 8) ? 3 : 0); }
@@ -70,7 +100,7 @@ __device__ __forceinline__ void load_vec(const float *msg, int Ep, int slot, flo
 {
 #pragma unroll
     for (int c = 0; c < Q / 4; ++c) {
-        const float4 t = *reinterpret_cast<const float4 *>(msg + ((c * Ep + slot) << 2));
+        const float4 t = *reinterpret_cast<const float4 *>(msg + ((c * Ep + (slot ^ c)) << 2));
         v[4 * c] = t.x;
         v[4 * c + 1] = t.y;
         v[4 * c + 2] = t.z;
@@ -126,7 +156,7 @@ __device__ __forceinline__ void store_out(float *msg, int Ep, int slot, float (&
     }
 #pragma unroll
     for (int c = 0; c < Q / 4; ++c)
-        *reinterpret_cast<float4 *>(msg + ((c * Ep + slot) << 2)) =
+        *reinterpret_cast<float4 *>(msg + ((c * Ep + (slot ^ c)) << 2)) =
             make_float4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
 }
 
@@ -202,21 +232,29 @@ __device__ __forceinline__ void vn_syndrome(const NbSched &sc, int e0, int e1, i
 
 // After the symbol phase's barrier: any check unsatisfied? Every syndrome word is
 // read and cleared (the next contributions come after the next check phase's barrier).
-__device__ __forceinline__ int syndrome_read_reset(uint32_t *synd, int nw)
+// The block-wide OR goes through one flag word per wave in the dynamic LDS (not
+// __syncthreads_or, whose static LDS word would move the messages off address 0);
+// a flag word is rewritten two barriers after its last read at the earliest.
+__device__ __forceinline__ int syndrome_read_reset(uint32_t *synd, int nw, int *flags)
 {
     int fail = 0;
     for (int w = threadIdx.x; w < nw; w += blockDim.x) {
         fail |= synd[w] != 0u;
         synd[w] = 0u;
     }
-    return __syncthreads_or(fail);
+    const int any = __any(fail);
+    if ((threadIdx.x & 63) == 0) flags[threadIdx.x >> 6] = any;
+    __syncthreads();
+    int r = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r |= flags[i];
+    return r;
 }
 
 // Entry a (symbol domain) of an edge's message lives at check-domain position
 // h*a. init: write v2c = L on every edge. Otherwise app = L + sum of the c2v
 // (nlist order), decision argmin app (first minimum), v2c = (app - c2v) - min.
 // Both add the new decision's syndrome contributions (vn_syndrome).
-template <int Q, int MB, int VD, int DC>
+template <int Q, int MB, int VD, int DC, bool GS>
 __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched &sc, const float *lam, uint8_t *dec,
                                         bool init, uint32_t *synd)
 {
@@ -241,23 +279,37 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
     // host chooses f with the XOR over every check's slots = 0, so each output
     // lands at exactly its own slot's swizzle. f spreads these gathers over the
     // LDS banks (nb_api.cpp nb_swizzled_coefficients).
+    // Byte offsets: (s << 4) ^ lambda((h*a) ^ f) with lambda XOR-linear (nb_lambda), so
+    // offset(a) = offset(a minus its lowest bit) ^ lambda(h * that bit): one v_xor per
+    // entry (the (p >> 2) * Ep + s form of the 2-mod-8 stride cost ~6 VALU per entry).
+    const int sh = sc.sh;
+    // In LDS the offsets are ds addresses: the message base (0: the kernel has no
+    // static LDS; any base aligned beyond the message bytes works) XOR-ed in once.
+    // In global memory (GS) they are byte offsets from msg.
+    const int xbase = GS ? 0 : (int)(unsigned)(uintptr_t)(LdsF *)msg;
+    auto lam_of = [sh](int p) { return (p << 2) ^ ((p >> 2) << sh); };
     auto addr = [&](int e, int (&ad)[Q]) {
         const int s = sc.vslot[e], hv = sc.vh[e], h1 = hv & 15, f = hv >> 4;
         const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
+        const int L[4] = {lam_of(h1), lam_of(h2), lam_of(h4), lam_of(h8)};
+        ad[0] = xbase ^ (s << 4) ^ lam_of(f);
 #pragma unroll
-        for (int a = 0; a < Q; ++a) {
-            const int p = ((a & 1) ? h1 : 0) ^ ((a & 2) ? h2 : 0) ^ ((a & 4) ? h4 : 0) ^ ((a & 8) ? h8 : 0) ^ f;
-            // (p >> 2) < 4 and Ep < 2^24: one full-rate v_mad_u32_u24 (the plain product
-            // compiled to quarter-rate v_mul_lo_u32 / v_mad_u64_u32, 64 per symbol-node pass)
-            ad[a] = (int)((__umul24((unsigned)(p >> 2), (unsigned)Ep) + (unsigned)s) << 2) + (p & 3);
-        }
+        for (int a = 1; a < Q; ++a) ad[a] = ad[a & (a - 1)] ^ L[__builtin_ctz(a)];
+    };
+    auto ld = [&](int off) -> float {
+        if constexpr (GS) return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(msg) + off);
+        else return *(LdsF *)(uintptr_t)(unsigned)off;
+    };
+    auto st = [&](int off, float x) {
+        if constexpr (GS) *reinterpret_cast<float *>(reinterpret_cast<char *>(msg) + off) = x;
+        else *(LdsF *)(uintptr_t)(unsigned)off = x;
     };
     int ad[Q];
     if (init) {
         for (int e = e0; e < e1; ++e) {
             addr(e, ad);
 #pragma unroll
-            for (int a = 0; a < Q; ++a) msg[ad[a]] = app[a];
+            for (int a = 0; a < Q; ++a) st(ad[a], app[a]);
         }
     } else if (VD > 0 && e1 - e0 <= VD) {
         // degree <= VD: each c2v is read once and kept in registers with its
@@ -271,7 +323,7 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
             if (k < deg) {
                 addr(e0 + k, ak[k]);
 #pragma unroll
-                for (int a = 0; a < Q; ++a) c[k][a] = msg[ak[k][a]];
+                for (int a = 0; a < Q; ++a) c[k][a] = ld(ak[k][a]);
             }
 #pragma unroll
         for (int k = 0; k < K; ++k)
@@ -299,14 +351,14 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
                     mn = fminf(mn, t[a]);
                 }
 #pragma unroll
-                for (int a = 0; a < Q; ++a) msg[ak[k][a]] = t[a] - mn;
+                for (int a = 0; a < Q; ++a) st(ak[k][a], t[a] - mn);
             }
         return;
     } else {
         for (int e = e0; e < e1; ++e) {
             addr(e, ad);
 #pragma unroll
-            for (int a = 0; a < Q; ++a) app[a] += msg[ad[a]];
+            for (int a = 0; a < Q; ++a) app[a] += ld(ad[a]);
         }
     }
     int best = 0;
@@ -325,18 +377,20 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
         float t[Q], mn = kInf;
 #pragma unroll
         for (int a = 0; a < Q; ++a) {
-            t[a] = app[a] - msg[ad[a]];
+            t[a] = app[a] - ld(ad[a]);
             mn = fminf(mn, t[a]);
         }
 #pragma unroll
-        for (int a = 0; a < Q; ++a) msg[ad[a]] = t[a] - mn;
+        for (int a = 0; a < Q; ++a) st(ad[a], t[a] - mn);
     }
 }
 
-template <int Q, int MB, int DC, int SRC>
+template <int Q, int MB, int DC, int SRC, bool GS>
 __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &g, int b, float *msg, float *lam,
-                                             uint8_t *dec, const NbSched &sc, int *red, uint32_t *synd)
+                                             uint8_t *dec, const NbSched &sc, int *red, uint32_t *synd,
+                                             EmsStamps &st)
 {
+    st.start();
     const int tid = threadIdx.x, nt = blockDim.x;
     const int N = g.N, M = g.M, Ep = sc.Ep;
     const uint64_t cw = a.first_cw + (uint64_t)b;
@@ -376,9 +430,10 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     }
     __syncthreads();
     // ---- initial messages v2c = L (stored at the check-domain position h*x), decisions argmin L ----
-    for (int v = tid; v < N; v += nt) vn_lane<Q, MB, 0, DC>(msg, Ep, v, sc, lam, dec, true, synd);
+    for (int v = tid; v < N; v += nt) vn_lane<Q, MB, 0, DC, GS>(msg, Ep, v, sc, lam, dec, true, synd);
     __syncthreads();
-    int fail = syndrome_read_reset(synd, (M + 3) / 4);
+    int fail = syndrome_read_reset(synd, (M + 3) / 4, red + 48);
+    EMS_LAP(0);
     int it = 0;
     // check lanes: in each wave, lanes 0-31 take 32 consecutive checks in mlist
     // order and lanes 32-63 the same checks reversed
@@ -409,12 +464,17 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
                 break;
             }
         }
+        EMS_LAP(1);
         __syncthreads();
+        EMS_LAP(2);
         // ---- symbol nodes: lane x = variable-domain symbol, reads c2v(x) at position h*x ----
         for (int v = tid; v < N && LDPC_EMS_EXP != 2; v += nt)
-            vn_lane<Q, MB, LDPC_EMS_VD, DC>(msg, Ep, v, sc, lam, dec, false, synd);
+            vn_lane<Q, MB, LDPC_EMS_VD, DC, GS>(msg, Ep, v, sc, lam, dec, false, synd);
+        EMS_LAP(3);
         __syncthreads();
-        if (LDPC_EMS_EXP != 3) fail = syndrome_read_reset(synd, (M + 3) / 4);
+        EMS_LAP(4);
+        if (LDPC_EMS_EXP != 3) fail = syndrome_read_reset(synd, (M + 3) / 4, red + 48);
+        EMS_LAP(5);
         ++it;
     }
 
@@ -439,18 +499,24 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         if (a.frame_res) a.frame_res[b] = make_int4(sums[0], sums[2], fail, it);
     }
     __syncthreads();
+    EMS_LAP(6);
+#ifdef LDPC_EMS_STAMPS
+    st.v[7] += 1;
+#endif
 }
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 
 // dynamic LDS: [msg 16*Ep f32 (ems_lds only)] [lam N*m f32] [dec N u8] [cn_d M u8]
-//              [vn N u32] [vslot E u16] [vh E u8] [synd ceil(M/4) u32]
+//              [vn N u32] [vslot E u16] [vh E u8] [synd ceil(M/4) u32] [red 48 i32] [flags 16 i32]
+// (no static LDS: the messages start at LDS address 0, so the symbol node's XOR-formed
+// offsets are its ds addresses as they are, without an add per entry)
 __host__ __device__ inline size_t aux_bytes(const NbDevGraph &g)
 {
     return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.M) +
            align16((size_t)g.N * 4) + align16((size_t)g.E * 2) + align16((size_t)g.E) +
-           align16((size_t)(g.M + 3) / 4 * 4);
+           align16((size_t)(g.M + 3) / 4 * 4) + (16 * 3 + 16) * 4;
 }
 
 template <int Q, int MB, int DC, int SRC, bool GSTATE, int THREADS>
@@ -458,7 +524,6 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
                                                             size_t slot_floats)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ int red[16 * 3];
     const int Ep = nb_ep(g);
     unsigned char *p = smem;
     float *msg;
@@ -481,6 +546,8 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
     uint8_t *vh = p;
     p += align16((size_t)g.E);
     uint32_t *synd = reinterpret_cast<uint32_t *>(p);   // check j: byte j & 3 of word j >> 2
+    p += align16((size_t)(g.M + 3) / 4 * 4);
+    int *red = reinterpret_cast<int *>(p);                // block_sum_n scratch, then the wave flags
     for (int w = threadIdx.x; w < (g.M + 3) / 4; w += blockDim.x) synd[w] = 0u;
     for (int j = threadIdx.x; j < g.M; j += blockDim.x) cn_d[j] = (uint8_t)(g.row_ptr[j + 1] - g.row_ptr[j]);
     for (int v = threadIdx.x; v < g.N; v += blockDim.x)
@@ -490,9 +557,14 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
         vh[e] = g.col_h[e];
     }
     __syncthreads();
-    const NbSched sc{Ep, g.M, cn_d, vn, vslot, vh};
+    const NbSched sc{Ep, g.M, nb_ep_log2(Ep) + 4, cn_d, vn, vslot, vh};
+    EmsStamps st;
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
-        ems_codeword<Q, MB, DC, SRC>(a, g, b, msg, lam, dec, sc, red, synd);
+        ems_codeword<Q, MB, DC, SRC, GSTATE>(a, g, b, msg, lam, dec, sc, red, synd, st);
+#ifdef LDPC_EMS_STAMPS
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < kEmsStampBlocks && (threadIdx.x >> 6) < 16)
+        for (int k = 0; k < 8; ++k) g_ems_stamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + k] = st.v[k];
+#endif
 }
 
 constexpr size_t kNbMaxLds = 160 * 1024;
@@ -565,7 +637,30 @@ hipError_t nb_launch(const NbDevGraph &g, const NbArgs &a, const NbChoice &ch, v
         grid = per_cu * num_cus;
         if (grid > a.batch) grid = a.batch;
     }
-    return ch.dc == 4 ? launch_dc<4>(g, a, ch, scratch, grid, s) : launch_dc<8>(g, a, ch, scratch, grid, s);
+#ifdef LDPC_EMS_STAMPS
+    const char *stamp_path = std::getenv("LDPC_EMS_STAMPS");
+    void *sp = nullptr;
+    if (stamp_path) {
+        hipError_t e = hipGetSymbolAddress(&sp, HIP_SYMBOL(g_ems_stamps));
+        if (e == hipSuccess) e = hipMemsetAsync(sp, 0, sizeof(g_ems_stamps), s);
+        if (e != hipSuccess) return e;
+    }
+#endif
+    const hipError_t err =
+        ch.dc == 4 ? launch_dc<4>(g, a, ch, scratch, grid, s) : launch_dc<8>(g, a, ch, scratch, grid, s);
+#ifdef LDPC_EMS_STAMPS
+    if (stamp_path && err == hipSuccess) {
+        static unsigned long long h[kEmsStampBlocks * 16 * 8];
+        hipError_t e = hipMemcpyAsync(h, sp, sizeof(h), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        if (FILE *f = std::fopen(stamp_path, "ab")) {
+            std::fwrite(h, sizeof(h[0]), sizeof(h) / sizeof(h[0]), f);
+            std::fclose(f);
+        }
+    }
+#endif
+    return err;
 }
 
 }  // namespace ldpc

@@ -141,7 +141,10 @@ static std::vector<uint8_t> nb_swizzled_coefficients(const ldpc_nb_graph &g, con
     std::vector<uint8_t> out(colh);
     if (g.q != ldpc::kNbQ || g.E == 0) return out;
     const int Q = g.q, N = g.N, M = g.M, DV = std::max(g.maxdv, 1);
-    const int Ep = (g.maxdc * g.M + 5) / 8 * 8 + 2;   // nb_ep
+    ldpc::NbDevGraph shape{};
+    shape.maxdc = g.maxdc;
+    shape.M = M;
+    const int lg = ldpc::nb_ep_log2(ldpc::nb_ep(shape));
     std::vector<uint8_t> f((size_t)g.maxdc * M, 0);
     std::vector<int> slot_v(f.size(), -1), slot_k(f.size(), 0);
     for (int v = 0; v < N; ++v)
@@ -157,7 +160,7 @@ static std::vector<uint8_t> nb_swizzled_coefficients(const ldpc_nb_graph &g, con
                 const int e = g.col_ptr[v] + k;
                 if (e >= g.col_ptr[v + 1]) continue;
                 const int sl = pslot[e], p = mul[(size_t)colh[e] * Q + a] ^ f[sl];
-                mx = std::max(mx, ++cnt[(((p >> 2) * Ep + sl) * 4 + (p & 3)) & 31]);
+                mx = std::max(mx, ++cnt[((((unsigned)sl << 4) ^ (unsigned)ldpc::nb_lambda(p, lg)) >> 2) & 31]);
             }
             tot += mx;
         }
