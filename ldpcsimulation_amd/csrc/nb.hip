@@ -218,16 +218,19 @@ __device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int di
 // into its checks' syndrome bytes (slot = k*M + j: check j = slot mod M, k < DC).
 // GF(16) sums are xors, so the order of the atomics does not matter.
 template <int DC>
+__device__ __forceinline__ void syndrome_edge(int M, int s, int hv, int d, uint32_t *synd)
+{
+    int j = s;
+#pragma unroll
+    for (int k = 1; k < DC; ++k) j -= j >= M ? M : 0;
+    const int h1 = hv & 15, h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
+    const int hd = ((d & 1) ? h1 : 0) ^ ((d & 2) ? h2 : 0) ^ ((d & 4) ? h4 : 0) ^ ((d & 8) ? h8 : 0);
+    if (hd) atomicXor(&synd[j >> 2], (uint32_t)hd << (8 * (j & 3)));
+}
+template <int DC>
 __device__ __forceinline__ void vn_syndrome(const NbSched &sc, int e0, int e1, int d, uint32_t *synd)
 {
-    for (int e = e0; e < e1; ++e) {
-        int j = sc.vslot[e];
-#pragma unroll
-        for (int k = 1; k < DC; ++k) j -= j >= sc.M ? sc.M : 0;
-        const int h1 = sc.vh[e] & 15, h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
-        const int hd = ((d & 1) ? h1 : 0) ^ ((d & 2) ? h2 : 0) ^ ((d & 4) ? h4 : 0) ^ ((d & 8) ? h8 : 0);
-        if (hd) atomicXor(&synd[j >> 2], (uint32_t)hd << (8 * (j & 3)));
-    }
+    for (int e = e0; e < e1; ++e) syndrome_edge<DC>(sc.M, sc.vslot[e], sc.vh[e], d, synd);
 }
 
 // After the symbol phase's barrier: any check unsatisfied? Every syndrome word is
@@ -288,14 +291,15 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
     // In global memory (GS) they are byte offsets from msg.
     const int xbase = GS ? 0 : (int)(unsigned)(uintptr_t)(LdsF *)msg;
     auto lam_of = [sh](int p) { return (p << 2) ^ ((p >> 2) << sh); };
-    auto addr = [&](int e, int (&ad)[Q]) {
-        const int s = sc.vslot[e], hv = sc.vh[e], h1 = hv & 15, f = hv >> 4;
+    auto addr_sh = [&](int s, int hv, int (&ad)[Q]) {
+        const int h1 = hv & 15, f = hv >> 4;
         const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
         const int L[4] = {lam_of(h1), lam_of(h2), lam_of(h4), lam_of(h8)};
         ad[0] = xbase ^ (s << 4) ^ lam_of(f);
 #pragma unroll
         for (int a = 1; a < Q; ++a) ad[a] = ad[a & (a - 1)] ^ L[__builtin_ctz(a)];
     };
+    auto addr = [&](int e, int (&ad)[Q]) { addr_sh(sc.vslot[e], sc.vh[e], ad); };
     auto ld = [&](int off) -> float {
         if constexpr (GS) return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(msg) + off);
         else return *(LdsF *)(uintptr_t)(unsigned)off;
@@ -317,11 +321,13 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
         constexpr int K = VD > 0 ? VD : 1;
         const int deg = e1 - e0;
         float c[K][Q];
-        int ak[K][Q];
+        int ak[K][Q], sk[K], hk[K];   // the edges' slots and coefficients, also for the syndrome
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (k < deg) {
-                addr(e0 + k, ak[k]);
+                sk[k] = sc.vslot[e0 + k];
+                hk[k] = sc.vh[e0 + k];
+                addr_sh(sk[k], hk[k], ak[k]);
 #pragma unroll
                 for (int a = 0; a < Q; ++a) c[k][a] = ld(ak[k][a]);
             }
@@ -340,7 +346,9 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
                 best = a;
             }
         dec[v] = (uint8_t)best;
-        vn_syndrome<DC>(sc, e0, e1, best, synd);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (k < deg) syndrome_edge<DC>(sc.M, sk[k], hk[k], best, synd);
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (k < deg) {
