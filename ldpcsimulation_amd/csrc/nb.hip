@@ -66,6 +66,11 @@ struct EmsStamps {
 };
 #define EMS_LAP(k) ((void)0)
 #endif
+// The table reads of each thread's first symbol node (vn_pre) are issued before the
+// check phase's barrier (1) or after it (0).
+#ifndef LDPC_EMS_HOIST
+#define LDPC_EMS_HOIST 1
+#endif
 // Symbol nodes of degree <= LDPC_EMS_VD keep their c2v in registers (0: re-read).
 #ifndef LDPC_EMS_VD
 #define LDPC_EMS_VD 2
@@ -253,67 +258,105 @@ __device__ __forceinline__ int syndrome_read_reset(uint32_t *synd, int nw, int *
     return r;
 }
 
-// Entry a (symbol domain) of an edge's message lives at check-domain position
-// h*a. init: write v2c = L on every edge. Otherwise app = L + sum of the c2v
-// (nlist order), decision argmin app (first minimum), v2c = (app - c2v) - min.
-// Both add the new decision's syndrome contributions (vn_syndrome).
-template <int Q, int MB, int VD, int DC, bool GS>
-__device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched &sc, const float *lam, uint8_t *dec,
-                                        bool init, uint32_t *synd)
+// Message addresses of the symbol node. Entry a of an edge is the check-domain
+// position h*a, stored at (h*a) ^ f, f = the slot's XOR swizzle (0 in the plain
+// layout). A check node works on its stored vectors as they are: ECN(P shifted by
+// f1, R shifted by f2) is ECN(P, R) shifted by f1 ^ f2 -- the same float sums, so
+// the same minima -- and the host chooses f with the XOR over every check's slots
+// = 0, so each output lands at exactly its own slot's swizzle. f spreads these
+// gathers over the LDS banks (nb_api.cpp nb_swizzled_coefficients).
+// Byte offsets: (s << 4) ^ lambda((h*a) ^ f) with lambda XOR-linear (nb_lambda), so
+// offset(a) = offset(a minus its lowest bit) ^ lambda(h * that bit): one v_xor per
+// entry (the (p >> 2) * Ep + s form of the 2-mod-8 stride cost ~6 VALU per entry).
+// In LDS the offsets are ds addresses: the message base (0: the kernel has no static
+// LDS; any base aligned beyond the message bytes works) XOR-ed in once. In global
+// memory (GS) they are byte offsets from msg.
+template <int Q, bool GS>
+struct MsgAddr {
+    float *msg;
+    int sh, xbase;
+    __device__ MsgAddr(float *m, int shift)
+        : msg(m), sh(shift), xbase(GS ? 0 : (int)(unsigned)(uintptr_t)(LdsF *)m) {}
+    __device__ int lam(int p) const { return (p << 2) ^ ((p >> 2) << sh); }
+    __device__ void edge(int s, int hv, int (&ad)[Q]) const
+    {
+        const int h1 = hv & 15, f = hv >> 4;
+        const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
+        const int L[4] = {lam(h1), lam(h2), lam(h4), lam(h8)};
+        ad[0] = xbase ^ (s << 4) ^ lam(f);
+#pragma unroll
+        for (int a = 1; a < Q; ++a) ad[a] = ad[a & (a - 1)] ^ L[__builtin_ctz(a)];
+    }
+    __device__ float ld(int off) const
+    {
+        if constexpr (GS) return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(msg) + off);
+        else return *(LdsF *)(uintptr_t)(unsigned)off;
+    }
+    __device__ void st(int off, float x) const
+    {
+        if constexpr (GS) *reinterpret_cast<float *>(reinterpret_cast<char *>(msg) + off) = x;
+        else *(LdsF *)(uintptr_t)(unsigned)off = x;
+    }
+};
+
+// The symbol node's table reads, which depend on no message: its bit LLRs, its
+// edge range and, for degree <= K, each edge's slot and coefficient. With one
+// symbol per thread they are issued before the check phase's barrier
+// (ems_codeword), so the symbol phase starts without two dependent LDS round trips.
+template <int Q, int K>
+struct VnPre {
+    float lv[4];            // the symbol's bit LLRs
+    int e0, e1;
+    int sk[K], hk[K];
+};
+
+template <int Q, int MB, int VD, bool GS>
+__device__ __forceinline__ void vn_pre(const MsgAddr<Q, GS> &ma, int v, const NbSched &sc, const float *lam,
+                                       VnPre<Q, (VD > 0 ? VD : 1)> &p)
 {
     static_assert(Q == 16 && MB == 4, "GF(16)");
     const float4 l4 = *reinterpret_cast<const float4 *>(lam + v * MB);
-    const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+    p.lv[0] = l4.x;
+    p.lv[1] = l4.y;
+    p.lv[2] = l4.z;
+    p.lv[3] = l4.w;
+    const uint32_t vp = sc.vn[v];
+    p.e0 = vp >> 8;
+    p.e1 = p.e0 + (vp & 255);
+    if (VD > 0 && p.e1 - p.e0 <= VD) {
+#pragma unroll
+        for (int k = 0; k < (VD > 0 ? VD : 1); ++k)
+            if (k < p.e1 - p.e0) {
+                p.sk[k] = sc.vslot[p.e0 + k];
+                p.hk[k] = sc.vh[p.e0 + k];
+            }
+    }
+}
+
+// Entry a (symbol domain) of an edge lives at check-domain position h*a. init:
+// write v2c = L on every edge. Otherwise app = L + sum of the c2v (nlist order),
+// decision argmin app (first minimum), v2c = (app - c2v) - min. Both add the new
+// decision's syndrome contributions (syndrome_edge).
+template <int Q, int MB, int VD, int DC, bool GS>
+__device__ __forceinline__ void vn_post(const MsgAddr<Q, GS> &ma, int v, const NbSched &sc, uint8_t *dec, bool init,
+                                        uint32_t *synd, VnPre<Q, (VD > 0 ? VD : 1)> &p)
+{
+    const int e0 = p.e0, e1 = p.e1;
     float app[Q];
 #pragma unroll
     for (int a = 0; a < Q; ++a) {
         float s = 0.0f;
 #pragma unroll
         for (int i = 0; i < MB; ++i)
-            if (((a >> i) & 1) != (lv[i] < 0.0f)) s += fabsf(lv[i]);   // oracle symbol_llr
+            if (((a >> i) & 1) != (p.lv[i] < 0.0f)) s += fabsf(p.lv[i]);   // oracle symbol_llr
         app[a] = s;
     }
-    const uint32_t vp = sc.vn[v];
-    const int e0 = vp >> 8, e1 = e0 + (vp & 255);
-    // entry a of the edge: check-domain position h*a, stored at (h*a) ^ f, f = the
-    // slot's XOR swizzle (0 in the plain layout). A check node works on its stored
-    // vectors as they are: ECN(P shifted by f1, R shifted by f2) is ECN(P, R)
-    // shifted by f1 ^ f2 -- the same float sums, so the same minima -- and the
-    // host chooses f with the XOR over every check's slots = 0, so each output
-    // lands at exactly its own slot's swizzle. f spreads these gathers over the
-    // LDS banks (nb_api.cpp nb_swizzled_coefficients).
-    // Byte offsets: (s << 4) ^ lambda((h*a) ^ f) with lambda XOR-linear (nb_lambda), so
-    // offset(a) = offset(a minus its lowest bit) ^ lambda(h * that bit): one v_xor per
-    // entry (the (p >> 2) * Ep + s form of the 2-mod-8 stride cost ~6 VALU per entry).
-    const int sh = sc.sh;
-    // In LDS the offsets are ds addresses: the message base (0: the kernel has no
-    // static LDS; any base aligned beyond the message bytes works) XOR-ed in once.
-    // In global memory (GS) they are byte offsets from msg.
-    const int xbase = GS ? 0 : (int)(unsigned)(uintptr_t)(LdsF *)msg;
-    auto lam_of = [sh](int p) { return (p << 2) ^ ((p >> 2) << sh); };
-    auto addr_sh = [&](int s, int hv, int (&ad)[Q]) {
-        const int h1 = hv & 15, f = hv >> 4;
-        const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
-        const int L[4] = {lam_of(h1), lam_of(h2), lam_of(h4), lam_of(h8)};
-        ad[0] = xbase ^ (s << 4) ^ lam_of(f);
-#pragma unroll
-        for (int a = 1; a < Q; ++a) ad[a] = ad[a & (a - 1)] ^ L[__builtin_ctz(a)];
-    };
-    auto addr = [&](int e, int (&ad)[Q]) { addr_sh(sc.vslot[e], sc.vh[e], ad); };
-    auto ld = [&](int off) -> float {
-        if constexpr (GS) return *reinterpret_cast<const float *>(reinterpret_cast<const char *>(msg) + off);
-        else return *(LdsF *)(uintptr_t)(unsigned)off;
-    };
-    auto st = [&](int off, float x) {
-        if constexpr (GS) *reinterpret_cast<float *>(reinterpret_cast<char *>(msg) + off) = x;
-        else *(LdsF *)(uintptr_t)(unsigned)off = x;
-    };
     int ad[Q];
     if (init) {
         for (int e = e0; e < e1; ++e) {
-            addr(e, ad);
+            ma.edge(sc.vslot[e], sc.vh[e], ad);
 #pragma unroll
-            for (int a = 0; a < Q; ++a) st(ad[a], app[a]);
+            for (int a = 0; a < Q; ++a) ma.st(ad[a], app[a]);
         }
     } else if (VD > 0 && e1 - e0 <= VD) {
         // degree <= VD: each c2v is read once and kept in registers with its
@@ -321,15 +364,13 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
         constexpr int K = VD > 0 ? VD : 1;
         const int deg = e1 - e0;
         float c[K][Q];
-        int ak[K][Q], sk[K], hk[K];   // the edges' slots and coefficients, also for the syndrome
+        int ak[K][Q];
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (k < deg) {
-                sk[k] = sc.vslot[e0 + k];
-                hk[k] = sc.vh[e0 + k];
-                addr_sh(sk[k], hk[k], ak[k]);
+                ma.edge(p.sk[k], p.hk[k], ak[k]);
 #pragma unroll
-                for (int a = 0; a < Q; ++a) c[k][a] = ld(ak[k][a]);
+                for (int a = 0; a < Q; ++a) c[k][a] = ma.ld(ak[k][a]);
             }
 #pragma unroll
         for (int k = 0; k < K; ++k)
@@ -348,7 +389,7 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
         dec[v] = (uint8_t)best;
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (k < deg) syndrome_edge<DC>(sc.M, sk[k], hk[k], best, synd);
+            if (k < deg) syndrome_edge<DC>(sc.M, p.sk[k], p.hk[k], best, synd);
 #pragma unroll
         for (int k = 0; k < K; ++k)
             if (k < deg) {
@@ -359,14 +400,14 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
                     mn = fminf(mn, t[a]);
                 }
 #pragma unroll
-                for (int a = 0; a < Q; ++a) st(ak[k][a], t[a] - mn);
+                for (int a = 0; a < Q; ++a) ma.st(ak[k][a], t[a] - mn);
             }
         return;
     } else {
         for (int e = e0; e < e1; ++e) {
-            addr(e, ad);
+            ma.edge(sc.vslot[e], sc.vh[e], ad);
 #pragma unroll
-            for (int a = 0; a < Q; ++a) app[a] += ld(ad[a]);
+            for (int a = 0; a < Q; ++a) app[a] += ma.ld(ad[a]);
         }
     }
     int best = 0;
@@ -381,16 +422,25 @@ __device__ __forceinline__ void vn_lane(float *msg, int Ep, int v, const NbSched
     vn_syndrome<DC>(sc, e0, e1, best, synd);
     if (init) return;
     for (int e = e0; e < e1; ++e) {
-        addr(e, ad);
+        ma.edge(sc.vslot[e], sc.vh[e], ad);
         float t[Q], mn = kInf;
 #pragma unroll
         for (int a = 0; a < Q; ++a) {
-            t[a] = app[a] - ld(ad[a]);
+            t[a] = app[a] - ma.ld(ad[a]);
             mn = fminf(mn, t[a]);
         }
 #pragma unroll
-        for (int a = 0; a < Q; ++a) st(ad[a], t[a] - mn);
+        for (int a = 0; a < Q; ++a) ma.st(ad[a], t[a] - mn);
     }
+}
+
+template <int Q, int MB, int VD, int DC, bool GS>
+__device__ __forceinline__ void vn_lane(const MsgAddr<Q, GS> &ma, int v, const NbSched &sc, const float *lam,
+                                        uint8_t *dec, bool init, uint32_t *synd)
+{
+    VnPre<Q, (VD > 0 ? VD : 1)> p;
+    vn_pre<Q, MB, VD, GS>(ma, v, sc, lam, p);
+    vn_post<Q, MB, VD, DC, GS>(ma, v, sc, dec, init, synd, p);
 }
 
 template <int Q, int MB, int DC, int SRC, bool GS>
@@ -438,7 +488,8 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     }
     __syncthreads();
     // ---- initial messages v2c = L (stored at the check-domain position h*x), decisions argmin L ----
-    for (int v = tid; v < N; v += nt) vn_lane<Q, MB, 0, DC, GS>(msg, Ep, v, sc, lam, dec, true, synd);
+    const MsgAddr<Q, GS> ma(msg, sc.sh);
+    for (int v = tid; v < N; v += nt) vn_lane<Q, MB, 0, DC, GS>(ma, v, sc, lam, dec, true, synd);
     __syncthreads();
     int fail = syndrome_read_reset(synd, (M + 3) / 4, red + 48);
     EMS_LAP(0);
@@ -447,6 +498,7 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     // order and lanes 32-63 the same checks reversed
     const int cdir = (tid >> 5) & 1, cpr = (nt >> 6) * 32;
     const int cj0 = (tid >> 6) * 32 + (tid & 31);
+    constexpr int KV = LDPC_EMS_VD > 0 ? LDPC_EMS_VD : 1;
     while (it < a.T && (!a.early_stop || fail)) {
         // ---- check nodes ----
         // the lane's first check, opaque per iteration: its message addresses are
@@ -473,11 +525,21 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
             }
         }
         EMS_LAP(1);
+        // the thread's first symbol: its table reads now, behind the check nodes
+        // still running
+        VnPre<Q, KV> pre;
+        if (LDPC_EMS_HOIST && tid < N) vn_pre<Q, MB, LDPC_EMS_VD, GS>(ma, tid, sc, lam, pre);
         __syncthreads();
         EMS_LAP(2);
         // ---- symbol nodes: lane x = variable-domain symbol, reads c2v(x) at position h*x ----
-        for (int v = tid; v < N && LDPC_EMS_EXP != 2; v += nt)
-            vn_lane<Q, MB, LDPC_EMS_VD, DC, GS>(msg, Ep, v, sc, lam, dec, false, synd);
+        if (LDPC_EMS_EXP != 2) {
+            if (tid < N) {
+                if (!LDPC_EMS_HOIST) vn_pre<Q, MB, LDPC_EMS_VD, GS>(ma, tid, sc, lam, pre);
+                vn_post<Q, MB, LDPC_EMS_VD, DC, GS>(ma, tid, sc, dec, false, synd, pre);
+            }
+            for (int v = tid + nt; v < N; v += nt)   // codes with more symbols than threads
+                vn_lane<Q, MB, LDPC_EMS_VD, DC, GS>(ma, v, sc, lam, dec, false, synd);
+        }
         EMS_LAP(3);
         __syncthreads();
         EMS_LAP(4);
