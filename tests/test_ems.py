@@ -249,11 +249,13 @@ def test_ems_waterfall(nbctx):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(2000, 1000, 2), (400, 200, 4), (300, 200, 3)],
-                         ids=["global_state_N2000", "dc8_kernel", "irregular_dc"])
+@pytest.mark.parametrize("shape", [(2000, 1000, 2), (400, 200, 4), (300, 200, 3), (600, 260, 2)],
+                         ids=["global_state_N2000", "dc8_kernel", "irregular_dc", "padded_stride_more_symbols"])
 def test_ems_other_kernels_bit_exact(shape):
-    """The global-memory message slot (codes beyond LDS), the DC=8 build (row degree 5..8)
-    and irregular row degrees, against the oracle."""
+    """The global-memory message slot (codes beyond LDS, more symbols than threads), the
+    DC=8 build (row degree 5..8), irregular row degrees, and a code whose position-major
+    slot count (maxdc*M = 1 300) pads to a 2 048-slot chunk stride with more symbols (600)
+    than the DC=8 build's 512 threads, against the oracle."""
     native = _native()
     codes = _codes()
     N, M, dv = shape
