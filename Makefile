@@ -118,10 +118,11 @@ fastvariant: $(OBJS)
 # Ping-pong kernel A/B variants: make ppvariant NAME=x VFLAGS="-DLDPC_PP_..." -> lib/variants/libldpc_hip_x.so
 ppvariant: $(OBJS)
 	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o $(CSRC)/rows_pp.hip
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o $(PPSRC)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/rows_pp.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o
 
+PPSRC ?= $(CSRC)/rows_pp.hip
 # EMS kernel A/B variants: make nbvariant NAME=x VFLAGS="-DLDPC_EMS_..." [NBSRC=file] -> lib/variants/libldpc_hip_x.so
 NBSRC ?= $(CSRC)/nb.hip
 nbvariant: $(OBJS)
