@@ -250,11 +250,13 @@ __device__ __forceinline__ int syndrome_read_reset(uint32_t *synd, int nw, int *
         fail |= synd[w] != 0u;
         synd[w] = 0u;
     }
+    // only the waves holding syndrome words have a flag to give (N=1000: two of 16)
+    const int nwv = (int)(blockDim.x >> 6), nf = nw < (int)blockDim.x ? (nw + 63) >> 6 : nwv;
     const int any = __any(fail);
-    if ((threadIdx.x & 63) == 0) flags[threadIdx.x >> 6] = any;
+    if ((threadIdx.x & 63) == 0 && (int)(threadIdx.x >> 6) < nf) flags[threadIdx.x >> 6] = any;
     __syncthreads();
     int r = 0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r |= flags[i];
+    for (int i = 0; i < nf; ++i) r |= flags[i];
     return r;
 }
 
