@@ -100,50 +100,55 @@ $(BINDIR)/decodeMGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 $(BINDIR)/decodeStochasticNGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BINDIR)
 	g++ $(CXXFLAGS) -D quantizeSamples -D quantizeProbabilities -D weightSyndromes -D saturateSamples -o $@ $< $(CLI_LINK)
 
-# Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> lib/variants/libldpc_hip_x.so
+# Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> ab/libldpc_hip_x.so
 variant:
-	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(NOSLP) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/api.o $(CSRC)/api.cpp
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(LIBDIR)/variants/obj_$(NAME)/kernels.o $(LIBDIR)/variants/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/graph.o
+	mkdir -p $(VARDIR)/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(NOSLP) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/api.o $(CSRC)/api.cpp
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
+	    $(VARDIR)/obj_$(NAME)/kernels.o $(VARDIR)/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/graph.o
 
-# Fast row kernel A/B variants: make fastvariant NAME=x VFLAGS="-DLDPC_FAST_..." -> lib/variants/libldpc_hip_x.so
+# Fast row kernel A/B variants: make fastvariant NAME=x VFLAGS="-DLDPC_FAST_..." -> ab/libldpc_hip_x.so
 fastvariant: $(OBJS)
-	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_fast.o $(CSRC)/rows_fast.hip
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(filter-out $(LIBDIR)/obj/rows_fast.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/rows_fast.o
+	mkdir -p $(VARDIR)/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/rows_fast.o $(CSRC)/rows_fast.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/rows_fast.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/rows_fast.o
 
-# Ping-pong kernel A/B variants: make ppvariant NAME=x VFLAGS="-DLDPC_PP_..." -> lib/variants/libldpc_hip_x.so
+# Ping-pong kernel A/B variants: make ppvariant NAME=x VFLAGS="-DLDPC_PP_..." -> ab/libldpc_hip_x.so
 ppvariant: $(OBJS)
-	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o $(PPSRC)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(filter-out $(LIBDIR)/obj/rows_pp.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/rows_pp.o
+	mkdir -p $(VARDIR)/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/rows_pp.o $(PPSRC)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/rows_pp.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/rows_pp.o
 
 PPSRC ?= $(CSRC)/rows_pp.hip
-# EMS kernel A/B variants: make nbvariant NAME=x VFLAGS="-DLDPC_EMS_..." [NBSRC=file] -> lib/variants/libldpc_hip_x.so
+# A/B variant libraries (bench.py / time_code.py / bench_ems.py --lib ab/libldpc_hip_NAME.so):
+# git-ignored; they ship to the GPU box only while they exist -- `make clean-ab` after an A/B session.
+VARDIR ?= ab
+clean-ab:
+	rm -rf $(VARDIR)
+# EMS kernel A/B variants: make nbvariant NAME=x VFLAGS="-DLDPC_EMS_..." [NBSRC=file] -> ab/libldpc_hip_x.so
 NBSRC ?= $(CSRC)/nb.hip
 nbvariant: $(OBJS)
-	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(NOSLP) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/nb.o $(NBSRC)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(filter-out $(LIBDIR)/obj/nb.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/nb.o
+	mkdir -p $(VARDIR)/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(NOSLP) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/nb.o $(NBSRC)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/nb.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/nb.o
 
-# GDBF kernel A/B variants: make gdbfvariant NAME=x VFLAGS="-DLDPC_GDBF_..." -> lib/variants/libldpc_hip_x.so
+# GDBF kernel A/B variants: make gdbfvariant NAME=x VFLAGS="-DLDPC_GDBF_..." -> ab/libldpc_hip_x.so
 gdbfvariant: $(OBJS)
-	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(NOSLP) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/gdbf.o $(CSRC)/gdbf.hip
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(filter-out $(LIBDIR)/obj/gdbf.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/gdbf.o
+	mkdir -p $(VARDIR)/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(NOSLP) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/gdbf.o $(CSRC)/gdbf.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/gdbf.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/gdbf.o
 
-# BP kernel A/B variants: make bpvariant NAME=x VFLAGS="-DLDPC_BP_..." -> lib/variants/libldpc_hip_x.so
+# BP kernel A/B variants: make bpvariant NAME=x VFLAGS="-DLDPC_BP_..." -> ab/libldpc_hip_x.so
 bpvariant: $(OBJS)
-	mkdir -p $(LIBDIR)/variants/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(LIBDIR)/variants/obj_$(NAME)/bp.o $(CSRC)/bp.hip
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(LIBDIR)/variants/libldpc_hip_$(NAME).so \
-	    $(filter-out $(LIBDIR)/obj/bp.o,$(OBJS)) $(LIBDIR)/variants/obj_$(NAME)/bp.o
+	mkdir -p $(VARDIR)/obj_$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/bp.o $(CSRC)/bp.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
+	    $(filter-out $(LIBDIR)/obj/bp.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/bp.o
 
 oracle:
 	$(MAKE) -f oracle/Makefile
@@ -155,7 +160,7 @@ ref:
 clean:
 	rm -rf $(LIBDIR) $(BINDIR) oracle/liboracle.so
 
-.PHONY: all oracle ref clean variant fastvariant ppvariant nbvariant
+.PHONY: all oracle ref clean clean-ab variant fastvariant ppvariant nbvariant gdbfvariant bpvariant
 
 # Host-code sanitizer build: graph.cpp (the Tanner-graph compiler)
 # and the CPU oracle under AddressSanitizer + UBSan, driven over code files.

@@ -26,11 +26,15 @@ step also all-reduces that round's per-frame counter sums over the ranks (RCCL,
 on the launch stream), the exchange the sharded SNR driver makes per round.
 
 roofline: the resource that bounds the row kernel is the LDS
-pipe. `achieved` = the LDS-array cycles the kernel's dataflow issues per
-launch at zero bank conflicts (from the row schedule: ds_read_b64 2 cycles,
-ds_write_b64 6 cycles per wave-instruction, MI355X_MICROARCH.md LDS table)
-divided by the average launch time (HIP events on the launch stream), in
-G LDS-cycles/s; `peak` = CUs x 2.4 GHz. The SURVEY §8(d) flooding HBM
+pipe. `achieved` = the ALGORITHMIC LDS-array cycles per launch -- per
+codeword-iteration E gathers of app, E scatters of c2v, E bit-side reads of
+c2v and N app writes, in 64-lane wave-instructions at their conflict-free
+costs (ds_read_b64 2, ds_write_b64 6 cycles, MI355X_MICROARCH.md LDS table),
+no padding -- divided by the average launch time (HIP events on the launch
+stream), in G LDS-cycles/s; `peak` = CUs x 2.4 GHz. Companions in
+`lds_model_alt`: `issued` (the wave-instructions the kernel issues, padding
+edges of its row slots included; the library reports its slot degrees) and
+`padded` (every row slot at the padded degree, the rounds 2-4 model). The SURVEY §8(d) flooding HBM
 message model (16E+4N bytes per codeword-iteration) is kept as `hbm_model`;
 it does not bound this kernel (messages never leave LDS), so its "fraction"
 exceeds 1. `traffic` = HBM bytes per launch of the headline kernel, measured
@@ -102,7 +106,19 @@ def parse(argv=None):
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="collective backend for N>1 (gloo + --share-device: rehearse N ranks on one GPU)")
     p.add_argument("--share-device", action="store_true", help="every rank on device 0 (rehearsal only)")
+    p.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                   help="A/B only: a kernel-choice option of the context (native.OPTIONS, e.g. rows64=fast)")
+    p.add_argument("--lib", default=None, help="A/B only: another build of the decoder library (make ppvariant ...)")
     return p.parse_args(argv)
+
+
+def parse_options(items) -> dict:
+    """--option NAME=VALUE items -> {name: value} (values: ints or native.OPTION_VALUES names)."""
+    out = {}
+    for it in items:
+        k, _, v = it.partition("=")
+        out[k.strip()] = int(v) if v.strip().lstrip("-").isdigit() else v.strip()
+    return out
 
 
 def cpu_share() -> int:
@@ -155,6 +171,7 @@ def live_traffic(args, kernel: str, precision: Optional[str] = None) -> dict:
     child = [sys.executable, os.path.abspath(__file__), "--steps", "1", "--warmup", "1", "--no-secondary",
              "--no-cpu-baseline", "--live-pmc", "off", "--precision", precision or args.precision, "--batch", str(args.batch),
              "--T", str(args.T), "--ebn0", str(args.ebn0), "--alpha", str(args.alpha), "--seed", str(args.seed)]
+    child += [f"--option={o}" for o in args.option] + (["--lib", args.lib] if args.lib else [])
     env = dict(os.environ, TMPDIR="/tmp")
     kib = {}
     with tempfile.TemporaryDirectory(prefix="ldpc_pmc_", dir="/tmp") as d:
@@ -323,40 +340,32 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def lds_model(si: dict, N: int) -> dict:
-    """LDS-array cycles per codeword-group iteration of the row kernel,
-    from its schedule: per iteration every row thread gathers dc app values
-    (ds_read_b64) and scatters dc c2v (ds_write_b64), every wave reads its
-    e_pad/64 bit-slot words (ds_read_b64) and writes its app slots (ds_write_b64).
-    One ds_*_b64 moves one fp64 value (C=1) or a codeword pair of fp32 (C=2)."""
-    rows = si["threads"] * si["rows_per_thread"]
-    w_gather = rows * si["dc"] / 64
-    w_scatter = rows * si["dc"] / 64
-    w_bitread = si["e_pad"] / 64
-    w_appwrite = si["threads"] * si["slots_per_thread"] / 64
-    cyc = {"check_gather": w_gather * LDS_CYC["ds_read_b64"], "check_scatter": w_scatter * LDS_CYC["ds_write_b64"],
-           "bit_read": w_bitread * LDS_CYC["ds_read_b64"], "app_write": w_appwrite * LDS_CYC["ds_write_b64"]}
-    return {"cycles_per_group_iter": sum(cyc.values()), "by_phase": cyc, "cw_per_group": si["cw_per_block"]}
-
-
-def lds_models_alt(si: dict, deg, N: int, kernel: str) -> dict:
-    """Two companions of lds_model's padded row-schedule model (the one `frac` uses, as
-    in rounds 2-3): `issued` -- the wave-instructions the kernel actually issues (the
-    ping-pong kernel's degree-aware slots, graph.h pp_row_slots: 7-edge check nodes in
-    768 of the 1024 row slots when every row of degree > 7 fits the other 256), and
-    `edges` -- the algorithmic minimum, E gathers + E scatters + E bit reads + N app
-    writes in 64-lane wave-instructions, no padding."""
-    deg = np.asarray(deg, dtype=np.int64)
-    rows = si["threads"] * si["rows_per_thread"]
-    split = (kernel == "rows_pp" and si["dc"] == 8 and si["rows_per_thread"] == 2 and si["threads"] == 512
-             and os.environ.get("LDPC_PP_ROWS", "") != "plain" and int((deg > 7).sum()) <= 256 and len(deg) <= rows)
-    slot_edges = (768 * 7 + 256 * 8) if split else rows * si["dc"]
+def lds_model(si: dict, E: int, N: int) -> dict:
+    """Algorithmic LDS-array cycles per codeword-group iteration of the flooding row
+    kernels: E gathers of app and E scatters of c2v by the check rows,
+    E reads of c2v and N writes of app by the bit nodes, in 64-lane wave-instructions
+    at their conflict-free costs, no padding. One ds_*_b64 moves one fp64 value
+    (C=1) or a codeword pair of fp32 (C=2), so a group is 1 or 2 codewords."""
     rd, wr = LDS_CYC["ds_read_b64"], LDS_CYC["ds_write_b64"]
-    issued = slot_edges / 64 * (rd + wr) + si["e_pad"] / 64 * rd + si["threads"] * si["slots_per_thread"] / 64 * wr
-    E = int(deg.sum())
-    edges = E / 64 * (rd + wr + rd) + N / 64 * wr
-    return {"issued": {"cycles_per_group_iter": issued, "degree_split": bool(split)},
-            "edges": {"cycles_per_group_iter": edges, "E": E}}
+    cyc = {"check_gather": E / 64 * rd, "check_scatter": E / 64 * wr, "bit_read": E / 64 * rd,
+           "app_write": N / 64 * wr}
+    return {"cycles_per_group_iter": sum(cyc.values()), "by_phase": cyc, "E": E, "N": N,
+            "cw_per_group": si["cw_per_block"]}
+
+
+def lds_models_alt(si: dict) -> dict:
+    """Two companions of the algorithmic model: `issued` -- the wave-instructions the
+    kernel issues (its row slots at the degree it compiles them with, padding edges
+    included: the library reports the check-edge slots, `issued_check_edges`, e.g.
+    768 x 7 + 256 x 8 for the ping-pong kernel's degree-aware slots, graph.h
+    pp_row_slots), and `padded` -- every row slot at the padded degree dc (the model
+    `frac` used in rounds 2-4)."""
+    rd, wr = LDS_CYC["ds_read_b64"], LDS_CYC["ds_write_b64"]
+    bit = si["e_pad"] / 64 * rd + si["threads"] * si["slots_per_thread"] / 64 * wr
+    rows = si["threads"] * si["rows_per_thread"]
+    return {"issued": {"cycles_per_group_iter": si["issued_check_edges"] / 64 * (rd + wr) + bit,
+                       "check_edge_slots": si["issued_check_edges"], "degree_split": si["dc_low"] > 0},
+            "padded": {"cycles_per_group_iter": rows * si["dc"] / 64 * (rd + wr) + bit}}
 
 
 def main():
@@ -380,7 +389,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.share_device:
         local = 0
-    if world > 1:
+    # Under torchrun a process group always exists, one rank included (a one-rank RCCL
+    # communicator): the per-step exchange and the max-over-ranks timing then run as they
+    # do at 8 ranks. Without torchrun (the driver's N=1 run) there is no collective.
+    distributed = "WORLD_SIZE" in os.environ
+    if distributed:
         torch.cuda.set_device(local)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -391,11 +404,13 @@ def main():
     coll_dev = "cuda" if args.backend == "nccl" else "cpu"
 
     from ldpcsimulation_amd import codes, native
+    if args.lib:
+        native.use_library(os.path.abspath(args.lib))
     alist = codes.ensure_80211n_1944()
     g = native.Graph.from_alist(alist)
-    row_deg = [len(r) for r in codes.read_alist(alist).rows]
     B = args.batch
     ctx = native.Context(g, local if world > 1 else 0, B)
+    ctx.set_options(parse_options(args.option))
     # A dedicated (non-default) torch stream: the library launches on it, so the
     # torch events below bracket exactly the decode kernel on its own stream.
     stream = torch.cuda.Stream()
@@ -410,7 +425,7 @@ def main():
         def step(k):
             first = (k * world + rank) * B
             ctx.sim_launch(args.ebn0, 0.5, cfg, args.seed, stream_id, first, B, frames_dev)
-            if world > 1 and args.backend == "nccl":
+            if distributed and args.backend == "nccl":
                 # the sharded driver's per-round exchange (sim.simulate_point): this round's
                 # counters summed over ranks, RCCL on the launch stream
                 part = frames_dev.sum(dim=0, dtype=torch.int64)
@@ -421,7 +436,7 @@ def main():
         torch.cuda.synchronize()
         ctx.read_counts(reset=True)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-        if world > 1:
+        if distributed:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -430,7 +445,7 @@ def main():
             step(args.warmup + k)
             ev[k][1].record(stream)
         torch.cuda.synchronize()
-        if world > 1:
+        if distributed:
             dist.barrier()
         elapsed = time.perf_counter() - t0
         kern_ms = [a.elapsed_time(b) for a, b in ev]
@@ -438,7 +453,7 @@ def main():
         cnt = ctx.read_counts(reset=True).as_array()
         t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         c = torch.from_numpy(np.append(cnt, redo)).to(coll_dev)
-        if world > 1:
+        if distributed:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(c)
         tot = c.cpu().numpy()
@@ -466,13 +481,13 @@ def main():
             si = ctx.row_sched_info(r["cfg"])
         except native.LdpcError:
             return out
-        m = lds_model(si, g.N)
+        m = lds_model(si, g.E, g.N)
         groups = B / si["cw_per_block"]
         cycles = m["cycles_per_group_iter"] * args.T * groups          # whole launch, all CUs
         n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
         achieved = cycles / avg_kernel_s / 1e9
         peak = n_cu * CLOCK_HZ / 1e9
-        alt = lds_models_alt(si, row_deg, g.N, info["kernel"])
+        alt = lds_models_alt(si)
         for k, v in alt.items():
             v["frac"] = v["cycles_per_group_iter"] * args.T * groups / avg_kernel_s / 1e9 / peak
         out.update({"bound": "lds", "achieved": achieved, "peak": peak, "unit": "G LDS-cycles/s",
@@ -529,6 +544,7 @@ def main():
                          **{k: v for k, v in rl.items() if k not in ("bound", "achieved", "peak", "unit", "frac")}},
             "fer": fer,
             "kernel_info": ctx.kernel_info(head["cfg"]),
+            "collective_backend": dist.get_backend() if distributed else None,
         }
         if sec is not None:
             rs = roofline(sec)
@@ -549,7 +565,7 @@ def main():
             except Exception as e:   # never lose the GPU line over the CPU leg
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

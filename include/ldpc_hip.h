@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 9
+#define LDPC_ABI_VERSION 10
 
 typedef enum {
     LDPC_OK = 0,
@@ -208,9 +208,8 @@ int  ldpc_sim_trace(ldpc_ctx *ctx, double ebn0_db, double R, const ldpc_decoder_
 /* Device time (ms) of the last decode kernel, from HIP events recorded on
  * the launch stream around it. Synchronises that stream. */
 int  ldpc_ctx_last_kernel_ms(ldpc_ctx *ctx, float *ms);
-/* Kernel chosen for a cfg ("lds" / "global") and its per-codeword LDS bytes.
- * The environment variable LDPC_FORCE_GLOBAL=1 (read at ldpc_ctx_create)
- * forces the global-memory kernel, for testing it on small codes. */
+/* Kernel chosen for a cfg ("rows_pp", "rows_fast", "rows", "lds", "flood",
+ * "global", "layered_*", "bp_*") and its per-codeword LDS bytes. */
 int  ldpc_ctx_kernel_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, char *name, int name_len,
                           int *lds_bytes, int *blocks_per_cu);
 /* Codewords of the last min-sum launch that the fast row kernel (fp64,
@@ -219,14 +218,51 @@ int  ldpc_ctx_kernel_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, char *name
  * the fast kernel). Diagnostic of the fast/exact split; synchronises the
  * stream. No reference counterpart (the reference has one exact path). */
 int  ldpc_ctx_redo_count(ldpc_ctx *ctx, int64_t *n);
-/* Shape of the row kernel ("rows"/"rows_fast") that decodes cfg, for the
- * on-chip (LDS) roofline model of bench.py: info[8] = {threads per block,
+/* Shape of the row kernel ("rows"/"rows_fast"/"rows_pp") that decodes cfg, for the
+ * on-chip (LDS) roofline model of bench.py: info[10] = {threads per block,
  * rows per thread, bit slots per thread, padded row degree, padded edge slots
- * e_pad, codewords per block, LDS bytes per block, blocks per CU}.
+ * e_pad, codewords per block, LDS bytes per block, blocks per CU, the low row
+ * degree of rows_pp's degree-aware slots (0: every slot runs the padded degree),
+ * check-node edge slots issued per codeword-iteration} (ABI 10: 10 entries).
  * LDPC_ERR_UNSUPPORTED when another kernel decodes cfg. Host-only, no device
  * call. No reference counterpart (diagnostic of decodeMinSum.cpp:247-263's
  * replacement). */
 int  ldpc_ctx_row_sched_info(ldpc_ctx *ctx, const ldpc_decoder_cfg *cfg, int32_t *info);
+
+/* ---- kernel-selection options (ABI 10) ------------------------------- */
+/* The library picks the kernel for a cfg by itself (the reference fixes its
+ * algorithm per binary at build time, C_implementations/Makefile:58-65). These
+ * per-context options override that choice for tests and A/B measurements;
+ * every alternative decodes bit-identically to the default (the GPU tests pin
+ * that). 0 is the library's own choice for every option; the library never
+ * reads them from the environment. Options take effect at the next launch. */
+typedef enum {
+    LDPC_OPT_ROWS64 = 1,           /* fp64 row graphs: 0 ping-pong (rows_pp), 1 rows_fast, 2 the row kernel   */
+    LDPC_OPT_ROWS32 = 2,           /* fp32 MS / NMS row graphs: 0 rows_pp pairs, 1 rows_fast pairs, 2 the row kernel */
+    LDPC_OPT_PP_SLOTS = 3,         /* rows_pp row slots: 0 degree-aware (when the code admits them), 1 plain  */
+    LDPC_OPT_KERNEL = 4,           /* generic kernel: 0 auto, 1 lds, 2 flood (persistent), 3 global           */
+    LDPC_OPT_FLOOD_MODE = 5,       /* codes beyond LDS: 0 one launch per phase, 1 the persistent kernel       */
+    LDPC_OPT_FLOOD_MSG = 6,        /* phase flooding messages: 0 packed row state, 1 the c2v array            */
+    LDPC_OPT_FLOOD_SPS_CHECK = 7,  /* phase flooding: resident slots per check-kernel step (0 = default)      */
+    LDPC_OPT_FLOOD_SPS_BIT = 8,    /* phase flooding: resident slots per bit-kernel step (0 = default)        */
+    LDPC_OPT_FLOOD_RESIDENT = 9,   /* phase flooding: resident codewords (0 = sized to the Infinity Cache)    */
+    LDPC_OPT_FLOOD_STREAMS = 10,   /* phase flooding: 2 = the resident set in two halves on two streams       */
+    LDPC_OPT_FLOOD_BPC = 11,       /* persistent flooding kernel: blocks per CU cap (0 = occupancy)           */
+    LDPC_OPT_LAYERED_BPC = 12,     /* global layered kernel: blocks per CU (0 = 1)                            */
+    LDPC_OPT_LAYERED_LDS_POS = 13, /* global layered kernel: positions kept in LDS + 1 (0 = as many as fit)   */
+    LDPC_OPT_LAYERED_ROWS64 = 14,  /* 512-thread global layered kernel, fp64 rows per pass: 1 or 2 (0 = 2)    */
+    LDPC_OPT_LAYERED_THREADS = 15, /* global layered kernel threads: 512 or 1024 (0 = 1024)                   */
+    LDPC_OPT_ROWS_BPC = 16,        /* row kernel (k_decode_rows): blocks per CU cap (0 = occupancy)           */
+    LDPC_OPT_FAST_BPC = 17,        /* rows_fast: blocks per CU cap (0 = occupancy)                            */
+    LDPC_OPT_BP_KERNEL = 18,       /* belief propagation: 0 bp_rows when the code fits, 1 the generic kernel  */
+    LDPC_OPT_GDBF_KERNEL = 19,     /* GDBF: 0 gdbf_rows when the code and flags fit, 1 the generic kernel     */
+    LDPC_OPT_EMS_THREADS = 20,     /* EMS (nb context), row degree 4: 0 = 1024 threads, 512                   */
+    LDPC_OPT_EMS_SWIZZLE = 21      /* EMS (nb context): 0 swizzled message slots, 1 the plain layout          */
+} ldpc_option;
+#define LDPC_OPT_COUNT 22
+/* LDPC_ERR_INVALID for an unknown option or a value outside its range. */
+int  ldpc_ctx_set_option(ldpc_ctx *ctx, int option, int value);
+int  ldpc_ctx_get_option(const ldpc_ctx *ctx, int option, int *value);
 
 /* ---- GDBF / NGDBF bit flipping (BASELINE config 4) --------------------- */
 /* src/decodeGDBF.cpp in its parallel-flip mode (mu = 1): syndrome check
@@ -339,6 +375,8 @@ int  ldpc_nb_ctx_read_counts(ldpc_nb_ctx *ctx, ldpc_nb_counts *out, int reset);
 int  ldpc_nb_ctx_last_kernel_ms(ldpc_nb_ctx *ctx, float *ms);
 /* "ems_lds" (messages in LDS) or "ems_global" (a global slot per workgroup). */
 int  ldpc_ems_kernel_info(ldpc_nb_ctx *ctx, char *name, int name_len, int *lds_bytes);
+/* (ABI 10) The EMS options of ldpc_option (LDPC_OPT_EMS_*); the others are refused. */
+int  ldpc_nb_ctx_set_option(ldpc_nb_ctx *ctx, int option, int value);
 
 /* Decode given channel samples y[batch][N*m] (float, host or device) with
  * bit LLRs 4y/n0. c: transmitted symbols [batch][N] or NULL (all-zero).

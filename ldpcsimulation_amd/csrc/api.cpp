@@ -80,7 +80,7 @@ struct ldpc_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     ldpc::AuxStream aux;          // second stream of the flooding phase launches (kernels.h)
     bool timed = false;
-    char force[16] = {0};        // LDPC_KERNEL=lds|flood|global (LDPC_FORCE_GLOBAL=1 = global), tests only
+    ldpc::Options opts;           // kernel-selection options (ldpc_ctx_set_option), tests and A/B only
     bool has_rs = false;
     ldpc::RowSched rs{};
     DevBuf sched;
@@ -104,6 +104,40 @@ int set_last_error(int code, const std::string &msg)
 {
     g_last_error = msg;
     return code;
+}
+
+static const Options kNoOptions{};
+static thread_local const Options *t_opts = nullptr;
+const Options &cur_opts() { return t_opts ? *t_opts : kNoOptions; }
+OptScope::OptScope(const Options &o) : prev_(t_opts) { t_opts = &o; }
+OptScope::~OptScope() { t_opts = prev_; }
+
+bool option_value_ok(int option, int v)
+{
+    switch (option) {
+    case LDPC_OPT_ROWS64:
+    case LDPC_OPT_ROWS32: return v >= 0 && v <= 2;
+    case LDPC_OPT_PP_SLOTS:
+    case LDPC_OPT_FLOOD_MODE:
+    case LDPC_OPT_FLOOD_MSG:
+    case LDPC_OPT_BP_KERNEL:
+    case LDPC_OPT_GDBF_KERNEL:
+    case LDPC_OPT_EMS_SWIZZLE: return v == 0 || v == 1;
+    case LDPC_OPT_KERNEL: return v >= 0 && v <= 3;
+    case LDPC_OPT_FLOOD_SPS_CHECK:
+    case LDPC_OPT_FLOOD_SPS_BIT: return v >= 0 && v <= 4;
+    case LDPC_OPT_FLOOD_RESIDENT: return v >= 0 && v <= 4096;
+    case LDPC_OPT_FLOOD_STREAMS: return v >= 0 && v <= 2;
+    case LDPC_OPT_FLOOD_BPC:
+    case LDPC_OPT_LAYERED_BPC:
+    case LDPC_OPT_ROWS_BPC:
+    case LDPC_OPT_FAST_BPC: return v >= 0 && v <= 64;
+    case LDPC_OPT_LAYERED_LDS_POS: return v >= 0 && v <= 65536;
+    case LDPC_OPT_LAYERED_ROWS64: return v >= 0 && v <= 2;
+    case LDPC_OPT_LAYERED_THREADS:
+    case LDPC_OPT_EMS_THREADS: return v == 0 || v == 512 || v == 1024;
+    default: return false;
+    }
 }
 }  // namespace ldpc
 
@@ -270,12 +304,6 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
     c->device = device;
     c->g = g;
     c->max_batch = max_batch;
-    {
-        const char *fg = std::getenv("LDPC_FORCE_GLOBAL");
-        const char *fk = std::getenv("LDPC_KERNEL");
-        if (fg && fg[0] == '1') std::snprintf(c->force, sizeof c->force, "global");
-        else if (fk) std::snprintf(c->force, sizeof c->force, "%s", fk);
-    }
     auto fail = [&](int rc) {
         ctx_free(c);
         return rc;
@@ -325,13 +353,10 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
 
     // Row-parallel schedule (the throughput kernel) when the graph fits it.
     {
-        // Two rows per thread in 512-thread blocks when M > 512 (two blocks per
-        // CU: their barriers overlap); LDPC_RPT=1|2 overrides (experiments).
         // Rows per thread: 1 up to 512 rows (512-thread blocks), 2 up to 1024 rows
-        // (512 threads, two blocks per CU: measured 1.13x over one 1024-thread
-        // block with 1 row per thread on the N=1944 code); LDPC_RPT=1|2 overrides.
-        int rpt = g->M <= 512 ? 1 : 2;
-        if (const char *er = std::getenv("LDPC_RPT")) rpt = std::max(1, std::min(2, std::atoi(er)));
+        // (512 threads, two blocks per CU: their barriers overlap; measured 1.13x
+        // over one 1024-thread block with 1 row per thread on the N=1944 code).
+        const int rpt = g->M <= 512 ? 1 : 2;
         int threads = ((((g->M + rpt - 1) / rpt) + 63) / 64) * 64;
         if (threads < 64) threads = 64;
         int dc = 0, cpt = 0;
@@ -446,6 +471,23 @@ int ldpc_ctx_synchronize(ldpc_ctx *c)
 
 void ldpc_ctx_destroy(ldpc_ctx *c) { ctx_free(c); }
 
+int ldpc_ctx_set_option(ldpc_ctx *c, int option, int value)
+{
+    if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    if (!ldpc::option_value_ok(option, value))
+        return set_err(LDPC_ERR_INVALID, "option %d: unknown, or value %d out of range", option, value);
+    c->opts.v[option] = value;
+    return LDPC_OK;
+}
+
+int ldpc_ctx_get_option(const ldpc_ctx *c, int option, int *value)
+{
+    if (!c || !value) return set_err(LDPC_ERR_INVALID, "null argument");
+    if (option <= 0 || option >= LDPC_OPT_COUNT) return set_err(LDPC_ERR_INVALID, "unknown option %d", option);
+    *value = c->opts.v[option];
+    return LDPC_OK;
+}
+
 // ----------------------------------------------------------------- helpers
 static bool is_device_ptr(const void *p)
 {
@@ -532,13 +574,19 @@ static int nms_setup(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, ldpc::DecodeArgs 
     return LDPC_OK;
 }
 
+// LDPC_OPT_KERNEL: the generic kernel a test forces (kernels.hip choose_kernel).
+static const char *forced_kernel(const ldpc_ctx *c)
+{
+    static const char *const names[] = {nullptr, "lds", "flood", "global"};
+    return names[c->opts.v[LDPC_OPT_KERNEL]];
+}
+
 static ldpc::KernelChoice select_kernel(const ldpc_ctx *c, bool f64, int schedule, int variant)
 {
+    const ldpc::OptScope os(c->opts);
     if (variant == LDPC_BP) return ldpc::bp_choose(c->dg, f64, c->g->E);
-    if (schedule == LDPC_LAYERED)
-        return ldpc::choose_layered(c->dg, f64, c->fs, c->ls, c->force[0] ? c->force : nullptr);
-    return ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, c->force[0] ? c->force : nullptr,
-                               c->has_fs ? &c->fs : nullptr);
+    if (schedule == LDPC_LAYERED) return ldpc::choose_layered(c->dg, f64, c->fs, c->ls, forced_kernel(c));
+    return ldpc::choose_kernel(c->dg, f64, c->has_rs ? &c->rs : nullptr, forced_kernel(c), c->has_fs ? &c->fs : nullptr);
 }
 
 static bool is_layered(const ldpc::KernelChoice &kc) { return kc.name[0] == 'l' && kc.name[1] == 'a'; }
@@ -547,8 +595,7 @@ static bool is_layered(const ldpc::KernelChoice &kc) { return kc.name[0] == 'l' 
 // pp_row_slots) when the code admits them, else the row kernel's.
 static const ldpc::RowSched &pp_sched(const ldpc_ctx *c)
 {
-    const char *e = std::getenv("LDPC_PP_ROWS");   // tests / A/B: "plain" = the row kernel's slots
-    if (e && std::strcmp(e, "plain") == 0) return c->rs;
+    if (c->opts.v[LDPC_OPT_PP_SLOTS] == 1) return c->rs;   // tests / A/B: the row kernel's slots
     return c->has_rs_pp ? c->rs_pp : c->rs;
 }
 
@@ -556,30 +603,28 @@ static const ldpc::RowSched &pp_sched(const ldpc_ctx *c)
 // exact re-decode (k_redo) of the codewords whose premise failed.
 //   fp64: the ping-pong kernel (rows_pp.hip: two codewords per 1024-thread block,
 //         check and bit waves overlapped) when the schedule fits it, else the
-//         one-codeword-per-block k_rows_fast (LDPC_ROWS=fast forces the latter);
+//         one-codeword-per-block k_rows_fast (LDPC_OPT_ROWS64 = 1 forces the latter);
 //   fp32: pairs as float2 -- MS and NMS with the verified reciprocal (a after
 //         nms_setup) -- on the ping-pong kernel (7.4 vs 8.8 ms per bench launch for
 //         the row kernel), on the pair instance of k_rows_fast with
-//         LDPC_ROWS32=fast, on the row kernel (kernels.hip k_decode_rows, fast and
-//         exact loops in one) with LDPC_ROWS32=rows and for everything else (OMS,
+//         LDPC_OPT_ROWS32 = 1, on the row kernel (kernels.hip k_decode_rows, fast and
+//         exact loops in one) with LDPC_OPT_ROWS32 = 2 and for everything else (OMS,
 //         codes the ping-pong schedule does not fit).
-// LDPC_ROWS=old keeps the row kernel for both.
+// LDPC_OPT_ROWS64 = 2 keeps the row kernel for fp64 too.
 enum class FastKind { none, pp, fast };
 static FastKind fast_kind(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
 {
-    const char *env = std::getenv("LDPC_ROWS");
-    if (env && std::strcmp(env, "old") == 0) return FastKind::none;
+    const int r64 = c->opts.v[LDPC_OPT_ROWS64], r32 = c->opts.v[LDPC_OPT_ROWS32];
+    if (f64 && r64 == 2) return FastKind::none;
     if (kc.name[0] != 'r' || !c->has_rs || ldpc::redo_lds_bytes(c->dg, f64) > 160 * 1024) return FastKind::none;
     const bool pp_ok = ldpc::rows_pp_supported(c->dg, pp_sched(c));
     if (f64) {
-        if (pp_ok && !(env && std::strcmp(env, "fast") == 0)) return FastKind::pp;
+        if (pp_ok && r64 == 0) return FastKind::pp;
         return ldpc::rows_fast_supported(c->rs, true) ? FastKind::fast : FastKind::none;
     }
     if (!ldpc::rows_fast_f32_ok(a)) return FastKind::none;
-    const char *e32 = std::getenv("LDPC_ROWS32");
-    if (e32 && std::strcmp(e32, "fast") == 0)
-        return ldpc::rows_fast_supported(c->rs, false) ? FastKind::fast : FastKind::none;
-    if (e32 && std::strcmp(e32, "rows") == 0) return FastKind::none;
+    if (r32 == 1) return ldpc::rows_fast_supported(c->rs, false) ? FastKind::fast : FastKind::none;
+    if (r32 == 2) return FastKind::none;
     return pp_ok ? FastKind::pp : FastKind::none;
 }
 static bool use_rows_fast(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f64, const ldpc::DecodeArgs &a)
@@ -593,15 +638,12 @@ static bool use_rows_pp(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f6
 
 // Flooding of codes beyond LDS: one launch per phase over an Infinity-Cache-
 // resident set (default; 1.5x the persistent kernel on DVB-S2) or the
-// persistent workgroup-per-codeword kernel (LDPC_FLOOD_MODE=persistent).
-static bool use_flood_phase()
-{
-    const char *e = std::getenv("LDPC_FLOOD_MODE");
-    return !(e && std::strcmp(e, "persistent") == 0);
-}
+// persistent workgroup-per-codeword kernel (LDPC_OPT_FLOOD_MODE = 1).
+static bool use_flood_phase(const ldpc_ctx *c) { return c->opts.v[LDPC_OPT_FLOOD_MODE] != 1; }
 
 static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int schedule)
 {
+    const ldpc::OptScope os(c->opts);
     const ldpc::KernelChoice kc = select_kernel(c, f64, schedule, a.variant);
     const bool layered = is_layered(kc);
     if (a.variant == ldpc::VARIANT_BP) {
@@ -621,14 +663,13 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         int per_cu = layered ? ldpc::layered_blocks_per_cu(f64, kc) : ldpc::blocks_per_cu(c->dg, f64, kc);
         // Global layered kernel: one codeword per CU by default, so the
         // resident state (DVB-S2: 256 x 583 KB) stays inside the 256 MiB
-        // Infinity Cache (2 per CU measured 1.5x slower); LDPC_LAYERED_BPC
+        // Infinity Cache (2 per CU measured 1.5x slower); LDPC_OPT_LAYERED_BPC
         // overrides (experiments).
         if (layered) {
-            int want = 1;
-            if (const char *e = std::getenv("LDPC_LAYERED_BPC")) want = std::max(1, std::atoi(e));
+            const int want = c->opts.v[LDPC_OPT_LAYERED_BPC] > 0 ? c->opts.v[LDPC_OPT_LAYERED_BPC] : 1;
             per_cu = std::min(per_cu, want);
-        } else if (const char *e = std::getenv("LDPC_FLOOD_BPC")) {   // global flooding kernel (experiments)
-            per_cu = std::min(per_cu, std::max(1, std::atoi(e)));
+        } else if (const int cap = c->opts.v[LDPC_OPT_FLOOD_BPC]) {   // global flooding kernel (experiments)
+            per_cu = std::min(per_cu, cap);
         }
         if (per_cu <= 0) per_cu = 1;
         gblocks = per_cu * c->num_cus;
@@ -663,7 +704,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         HIP_TRY(ldpc::launch_redo(c->dg, a, f64, (const unsigned *)c->redo.p, c->stream, c->num_cus));
     } else if (layered) {
         HIP_TRY(ldpc::launch_layered(c->dg, a, f64, kc, c->fs, c->ls, c->gscratch.p, gblocks, c->stream));
-    } else if (kc.name[0] == 'f' && use_flood_phase())
+    } else if (kc.name[0] == 'f' && use_flood_phase(c))
         HIP_TRY(ldpc::launch_flood_phase(c->dg, c->fs, a, f64, kc, c->gscratch.p, c->gscratch.n, c->stream, &c->aux));
     else
         HIP_TRY(ldpc::launch_decode(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->stream,
@@ -969,9 +1010,16 @@ int ldpc_ctx_row_sched_info(ldpc_ctx *c, const ldpc_decoder_cfg *cfg, int32_t *i
     fill_common(a, c, cfg, 1);
     rc = nms_setup(c, cfg, a);   // fp32 NMS: whether the verified reciprocal (and so the fast kernels) applies
     if (rc) return rc;
+    info[8] = 0;
+    info[9] = c->rs.threads * c->rs.rpt * c->rs.dc;   // check edge slots issued per codeword-iteration
     if (use_rows_pp(c, kc, f64, a)) {   // one 1024-thread block per CU
-        info[6] = ldpc::rows_pp_lds_bytes(c->dg, pp_sched(c));
+        const ldpc::RowSched &rs = pp_sched(c);
+        info[6] = ldpc::rows_pp_lds_bytes(c->dg, rs);
         info[7] = 1;
+        info[8] = rs.dc_low;
+        // degree-aware slots (rows_pp.hip k_rows_pp SPLIT): every row-0 slot and the row-1 slots of
+        // threads >= threads/2 run a dc_low-edge check node, the other row-1 slots a dc-edge one
+        if (rs.dc_low) info[9] = (rs.threads + rs.threads / 2) * rs.dc_low + (rs.threads / 2) * rs.dc;
     }
     return LDPC_OK;
 }
@@ -1059,6 +1107,7 @@ static void gdbf_fill(ldpc::GdbfArgs &a, ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, 
 
 static int gdbf_run(ldpc_ctx *c, const ldpc::GdbfArgs &a, bool f64)
 {
+    const ldpc::OptScope os(c->opts);
     const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, f64, a.flags, c->g->maxdv, c->g->maxdc);
     int slots = 0;
     if (ch.slot_bytes) {
@@ -1223,6 +1272,7 @@ int ldpc_gdbf_kernel_info(ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, char *name, int
     int rc = gdbf_check_cfg(cfg);
     if (rc) return rc;
     if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
+    const ldpc::OptScope os(c->opts);
     const ldpc::GdbfChoice ch = ldpc::gdbf_choose(c->dg, cfg->precision == LDPC_F64, cfg->flags, c->g->maxdv, c->g->maxdc);
     if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", ch.name);
     if (lds_bytes) *lds_bytes = ch.lds_bytes;

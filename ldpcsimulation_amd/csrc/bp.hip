@@ -417,11 +417,7 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
     }
 }
 
-static bool bp_rows_forced_off()
-{
-    const char *e = std::getenv("LDPC_BP_KERNEL");
-    return e && std::strcmp(e, "generic") == 0;
-}
+static bool bp_rows_forced_off() { return opt(LDPC_OPT_BP_KERNEL) == 1; }
 
 constexpr size_t kBpMaxLds = 160 * 1024;
 

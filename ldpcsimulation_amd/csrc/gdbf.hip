@@ -680,11 +680,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
 constexpr size_t kGdbfMaxLds = 64 * 1024;
 constexpr int kGdbfRowsUnsupported = GDBF_SEQUENTIAL | GDBF_MODESWITCH | GDBF_QPROB;
 
-static bool gdbf_rows_forced_off()
-{
-    const char *e = std::getenv("LDPC_GDBF_KERNEL");
-    return e && std::strcmp(e, "generic") == 0;
-}
+static bool gdbf_rows_forced_off() { return opt(LDPC_OPT_GDBF_KERNEL) == 1; }
 
 GdbfChoice gdbf_choose(const DevGraph &g, bool f64, int flags, int maxdv, int maxdc)
 {

@@ -1,5 +1,6 @@
 // kernels.h -- internal launch interface between api.cpp and kernels.hip.
 #pragma once
+#include "options.h"
 #include <hip/hip_runtime.h>
 #include <cstdint>
 

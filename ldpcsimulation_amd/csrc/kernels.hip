@@ -852,23 +852,21 @@ __global__ __launch_bounds__(256) void k_flood_account(DecodeArgs a, int b0, int
 }
 
 // Messages between the phases: the packed row state (default) or the c2v
-// array (LDPC_FLOOD_MSG=c2v). The packed bit phase is built for column degrees
+// array (option LDPC_OPT_FLOOD_MSG = 1). The packed bit phase is built for column degrees
 // up to 32 (k_flood_bit_packed<F, 8|16|32>); a code with a heavier column takes
 // the c2v array, whose bit phase has an any-degree instance (DV = 0).
 constexpr int kFloodPackedMaxDv = 32;
 static bool flood_packed(const FloodSched &fs)
 {
     if (fs.dv > kFloodPackedMaxDv) return false;
-    const char *e = std::getenv("LDPC_FLOOD_MSG");
-    return !(e && std::strcmp(e, "c2v") == 0);
+    return opt(LDPC_OPT_FLOOD_MSG) != 1;
 }
 
-// Resident slots per step of the check (LDPC_FLOOD_SPS_CHECK) and bit
-// (LDPC_FLOOD_SPS_BIT) phase kernels.
+// Resident slots per step of the check (LDPC_OPT_FLOOD_SPS_CHECK) and bit
+// (LDPC_OPT_FLOOD_SPS_BIT) phase kernels.
 static int flood_sps(bool check, const FloodSched &fs)
 {
-    const char *e = std::getenv(check ? "LDPC_FLOOD_SPS_CHECK" : "LDPC_FLOOD_SPS_BIT");
-    if (e) return std::max(1, std::atoi(e));
+    if (const int v = opt(check ? LDPC_OPT_FLOOD_SPS_CHECK : LDPC_OPT_FLOOD_SPS_BIT)) return v;
     return check || flood_packed(fs) ? 1 : 2;   // packed bit phase: 1 (2 204 vs 2 124 Mbit/s fp32)
 }
 
@@ -878,12 +876,12 @@ static int flood_sps(bool check, const FloodSched &fs)
 // the slot alone). Measured on DVB-S2 R1/2 with packed messages (4096
 // codewords, T=50): fp32 K = 96/112/128/144 -> 2277/2307/2331/2310 Mbit/s,
 // fp64 K = 64/80/96/128 -> 1520/1508/1487/1401 -- best near 110 MB touched.
-// LDPC_FLOOD_RESIDENT overrides.
+// LDPC_OPT_FLOOD_RESIDENT overrides.
 constexpr size_t kFloodPhaseExtra = 65536;   // per-slot counters after the slots (3 ints per slot)
 static int flood_phase_resident(size_t slot_bytes, size_t touched, size_t gscratch_bytes)
 {
     long k = (long)((112ull << 20) / touched);
-    if (const char *e = std::getenv("LDPC_FLOOD_RESIDENT")) k = std::atol(e);
+    if (const int v = opt(LDPC_OPT_FLOOD_RESIDENT)) k = v;
     if (k > 4096) k = 4096;
     const long cap = (long)((gscratch_bytes - kFloodPhaseExtra) / slot_bytes);
     if (k > cap) k = cap;
@@ -991,13 +989,9 @@ struct FloodHalf {
 // boundaries and its small init / finish / accounting launches overlap the other
 // half's phase kernels. The single stream is 95 % busy already
 // (profiles/r03_dvbs2_flood_gaps.json).
-// LDPC_FLOOD_STREAMS=2 (opt-in): measured +6 % while the bit kernel's loads were
+// LDPC_OPT_FLOOD_STREAMS = 2 (opt-in): measured +6 % while the bit kernel's loads were
 // serialised, 7 % slower once they are batched (1 855 vs 2 000 Mbit/s).
-static bool flood_two_streams()
-{
-    const char *e = std::getenv("LDPC_FLOOD_STREAMS");
-    return e && std::atoi(e) == 2;
-}
+static bool flood_two_streams() { return opt(LDPC_OPT_FLOOD_STREAMS) == 2; }
 
 template <typename F, int SRC>
 static hipError_t launch_flood_phase_t(const DevGraph &g, const FloodSched &fs, const DecodeArgs &a,
@@ -1922,8 +1916,8 @@ static hipError_t launch_rows_t(const DevGraph &g, const RowSched &rs, const Dec
     int per_cu = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kc.threads, kc.lds_bytes);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    if (const char *cap = std::getenv("LDPC_BLOCKS_PER_CU"))   // diagnostic: fewer resident blocks
-        if (std::atoi(cap) >= 1 && std::atoi(cap) < per_cu) per_cu = std::atoi(cap);
+    if (const int cap = opt(LDPC_OPT_ROWS_BPC))   // diagnostic: fewer resident blocks
+        if (cap < per_cu) per_cu = cap;
     const int ngrp = (a.batch + C - 1) / C;
     int grid = per_cu * num_cus;
     if (grid > ngrp) grid = ngrp;
@@ -2035,33 +2029,25 @@ int blocks_per_cu(const DevGraph &g, bool f64, const KernelChoice &kc)
 
 // ---------------------------------------------------------------- layered
 // Layered positions (of np) the global kernel keeps in LDS: as many as fit
-// beside the static LDS (LDPC_LAYERED_LDS_POS caps it; 0 = all in the slot).
+// beside the static LDS (LDPC_OPT_LAYERED_LDS_POS = P + 1 caps it at P; 1 = all in the slot).
 static int layered_lds_positions(int np, size_t fsz)
 {
     long P = (long)((kMaxLds - 4096) / fsz) - 1;
-    if (const char *e = std::getenv("LDPC_LAYERED_LDS_POS")) P = std::min(P, std::max(0L, std::atol(e)));
+    if (const int v = opt(LDPC_OPT_LAYERED_LDS_POS)) P = std::min(P, (long)(v - 1));
     return (int)std::min(P, (long)np);
 }
 
 // Rows per thread per pass: the global kernel batches R rows' gathers
 // (latency of the L2/Infinity Cache), the LDS kernel does one row at a time.
-// fp64: 2 (DVB-S2 1 530 vs 1 470 Mbit/s at 1 and 1 425 at 3); LDPC_LAYERED_R64=1 for A/B.
-static int layered_r64()
-{
-    const char *e = std::getenv("LDPC_LAYERED_R64");
-    return (e && std::atoi(e) == 1) ? 1 : 2;
-}
+// fp64: 2 (DVB-S2 1 530 vs 1 470 Mbit/s at 1 and 1 425 at 3); LDPC_OPT_LAYERED_ROWS64 = 1 for A/B.
+static int layered_r64() { return opt(LDPC_OPT_LAYERED_ROWS64) == 1 ? 1 : 2; }
 // Threads of the global layered kernel: 1024 (4 waves per SIMD at <= 128 VGPRs,
 // R = 2 rows per thread per pass in fp32, 1 in fp64) -- DVB-S2 T=50: fp32 59.4 ->
 // 42.7 ms, fp64 87.4 -> 74.2 ms per 2,048 codewords against 512 threads (2 waves
 // per SIMD at ~256 VGPRs, R = 4 / 2: the same rows in flight per pass, half the
-// waves to hide the L2 / Infinity Cache latency); LDPC_LAYERED_THREADS=512 keeps
-// the latter.
-static int layered_nt()
-{
-    const char *e = std::getenv("LDPC_LAYERED_THREADS");
-    return (e && std::atoi(e) == 512) ? 512 : 1024;
-}
+// waves to hide the L2 / Infinity Cache latency); LDPC_OPT_LAYERED_THREADS = 512
+// keeps the latter.
+static int layered_nt() { return opt(LDPC_OPT_LAYERED_THREADS) == 512 ? 512 : 1024; }
 static int layered_rows_per_pass(bool global, bool f64)
 {
     if (!global) return 1;

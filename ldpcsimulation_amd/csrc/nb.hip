@@ -647,13 +647,12 @@ NbChoice nb_choose(const NbDevGraph &g, int maxdc)
     ch.dc = maxdc <= 4 ? 4 : 8;
     // DC = 4: 1024 threads (4 waves per SIMD; 128 VGPRs, spills only around
     // the codeword loop: 8.12 vs 8.00 Gbit/s at 2.0 dB with 512),
-    // LDPC_EMS_THREADS=512 the other build. DC = 8: 512 (its check node needs
+    // LDPC_OPT_EMS_THREADS = 512 the other build. DC = 8: 512 (its check node needs
     // ~180 VGPRs). LDS allows one workgroup per CU either way.
     ch.threads = 512;
     if (ch.dc == 4) {
         ch.threads = 1024;
-        const char *e = std::getenv("LDPC_EMS_THREADS");
-        if (e && std::atoi(e) == 512) ch.threads = 512;
+        if (opt(LDPC_OPT_EMS_THREADS) == 512) ch.threads = 512;
     }
     const size_t aux = aux_bytes(g), msgb = align16((size_t)nb_ep(g) * g.q * 4);
     if (maxdc > kNbMaxDc || aux > kNbMaxLds || nb_ep(g) > 65535 || g.N > 65535) {

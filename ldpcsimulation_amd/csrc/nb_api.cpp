@@ -116,14 +116,11 @@ struct ldpc_nb_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     const uint8_t *col_h_swz = nullptr;   // device: col_h with the slot swizzles (nb_swizzled_coefficients)
+    ldpc::Options opts;                   // kernel-selection options (ldpc_nb_ctx_set_option)
 };
 
-// LDPC_EMS_SWIZZLE=0 keeps the plain message layout (A/B).
-static bool nb_swizzle_enabled()
-{
-    const char *e = std::getenv("LDPC_EMS_SWIZZLE");
-    return !(e && std::atoi(e) == 0);
-}
+// LDPC_OPT_EMS_SWIZZLE = 1 keeps the plain message layout (A/B).
+static bool nb_swizzle_enabled() { return ldpc::opt(LDPC_OPT_EMS_SWIZZLE) != 1; }
 
 // XOR swizzles of the message slots for the symbol-node gathers of nb.hip
 // (vn_lane: entry a of an edge is read at check-domain position (h*a) ^ f,
@@ -485,6 +482,7 @@ static void add_counts(ldpc_nb_counts *acc, const unsigned long long *after, con
 
 static int run(ldpc_nb_ctx *c, const ldpc::NbArgs &a)
 {
+    const ldpc::OptScope os(c->opts);
     const ldpc::NbChoice ch = ldpc::nb_choose(c->dg, c->g->maxdc);
     int slots = 0;
     if (ch.slot_bytes) {
@@ -679,9 +677,20 @@ int ldpc_nb_ctx_last_kernel_ms(ldpc_nb_ctx *c, float *ms)
 int ldpc_ems_kernel_info(ldpc_nb_ctx *c, char *name, int name_len, int *lds_bytes)
 {
     if (!c) return err(LDPC_ERR_INVALID, "ctx is null");
+    const ldpc::OptScope os(c->opts);
     const ldpc::NbChoice ch = ldpc::nb_choose(c->dg, c->g->maxdc);
     if (name && name_len > 0) std::snprintf(name, (size_t)name_len, "%s", ch.name);
     if (lds_bytes) *lds_bytes = ch.lds_bytes;
+    return LDPC_OK;
+}
+
+int ldpc_nb_ctx_set_option(ldpc_nb_ctx *c, int option, int value)
+{
+    if (!c) return err(LDPC_ERR_INVALID, "ctx is null");
+    if (option != LDPC_OPT_EMS_THREADS && option != LDPC_OPT_EMS_SWIZZLE)
+        return err(LDPC_ERR_INVALID, "option %d is not an EMS option", option);
+    if (!ldpc::option_value_ok(option, value)) return err(LDPC_ERR_INVALID, "option %d: value %d out of range", option, value);
+    c->opts.v[option] = value;
     return LDPC_OK;
 }
 

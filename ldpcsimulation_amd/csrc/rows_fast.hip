@@ -372,7 +372,7 @@ static hipError_t launch_fast_t(const DevGraph &g, const RowSched &rs, const Dec
     int per_cu = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, rs.threads, lds);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    if (const char *eb = std::getenv("LDPC_FAST_BPC")) per_cu = std::max(1, std::min(per_cu, std::atoi(eb)));   // experiments
+    if (const int cap = opt(LDPC_OPT_FAST_BPC)) per_cu = std::min(per_cu, cap);   // experiments
     const int ngrp = (a.batch + C - 1) / C;
     int grid = per_cu * num_cus;
     if (grid > ngrp) grid = ngrp;

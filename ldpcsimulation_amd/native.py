@@ -14,15 +14,44 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "lib", "libldpc_hip.so")
-# A/B experiments: LDPC_LIB=<name> loads lib/variants/libldpc_hip_<name>.so (built by `make variant`)
-if os.environ.get("LDPC_LIB"):
-    LIB_PATH = os.path.join(_PKG, "lib", "variants", f"libldpc_hip_{os.environ['LDPC_LIB']}.so")
 
 LDPC_OK = 0
 MS, NMS, OMS, BP = 0, 1, 2, 3
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 9
+ABI_VERSION = 10
+# Kernel-selection options (include/ldpc_hip.h ldpc_option): tests and A/B runs set
+# them per context through the ABI; the library never reads the environment.
+OPTIONS = {"rows64": 1, "rows32": 2, "pp_slots": 3, "kernel": 4, "flood_mode": 5, "flood_msg": 6,
+           "flood_sps_check": 7, "flood_sps_bit": 8, "flood_resident": 9, "flood_streams": 10, "flood_bpc": 11,
+           "layered_bpc": 12, "layered_lds_pos": 13, "layered_rows64": 14, "layered_threads": 15,
+           "rows_bpc": 16, "fast_bpc": 17, "bp_kernel": 18, "gdbf_kernel": 19, "ems_threads": 20,
+           "ems_swizzle": 21}
+# symbolic values of the kernel-choice options
+OPTION_VALUES = {"rows64": {"pp": 0, "fast": 1, "rows": 2}, "rows32": {"pp": 0, "fast": 1, "rows": 2},
+                 "pp_slots": {"split": 0, "plain": 1}, "kernel": {"auto": 0, "lds": 1, "flood": 2, "global": 3},
+                 "flood_mode": {"phase": 0, "persistent": 1}, "flood_msg": {"packed": 0, "c2v": 1},
+                 "bp_kernel": {"rows": 0, "generic": 1}, "gdbf_kernel": {"rows": 0, "generic": 1},
+                 "ems_swizzle": {"on": 0, "off": 1}}
+
+
+def option_id(name) -> int:
+    return name if isinstance(name, int) else OPTIONS[name]
+
+
+def option_value(name, value) -> int:
+    if isinstance(value, str) and not isinstance(name, int):
+        return OPTION_VALUES[name][value]
+    return int(value)
+
+
+def use_library(path: str):
+    """Load another build of the library (A/B variants; `bench.py --lib`). Only before
+    the first call into the library; the product path is LIB_PATH."""
+    global LIB_PATH
+    if _lib is not None and os.path.abspath(path) != os.path.abspath(LIB_PATH):
+        raise RuntimeError("the decoder library is already loaded")
+    LIB_PATH = path
 _STATUS = {0: "OK", -1: "INVALID", -2: "NOMEM", -3: "DEVICE", -4: "UNSUPPORTED", -5: "IO", -6: "GRAPH"}
 
 
@@ -188,6 +217,9 @@ def lib():
         "ldpc_ctx_kernel_info": ([vp, C.POINTER(_Cfg), C.c_char_p, i32, C.POINTER(i32), C.POINTER(i32)], i32),
         "ldpc_ctx_redo_count": ([vp, C.POINTER(C.c_int64)], i32),
         "ldpc_ctx_row_sched_info": ([vp, C.POINTER(_Cfg), vp], i32),
+        "ldpc_ctx_set_option": ([vp, i32, i32], i32),
+        "ldpc_ctx_get_option": ([vp, i32, C.POINTER(i32)], i32),
+        "ldpc_nb_ctx_set_option": ([vp, i32, i32], i32),
         "ldpc_gdbf_decode_batch": ([vp, vp, vp, i32, C.POINTER(_GdbfCfg), vp, vp, vp, C.POINTER(Counts)], i32),
         "ldpc_gdbf_sim_launch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp], i32),
         "ldpc_gdbf_sim_batch": ([vp, dbl, dbl, C.POINTER(_GdbfCfg), u64, u32, u64, i32, vp, C.POINTER(Counts)],
@@ -226,7 +258,7 @@ EXPORTED = ["ldpc_abi_version", "ldpc_f64_nms_fast_division", "ldpc_last_error",
             "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
             "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",
             "ldpc_sim_batch", "ldpc_sim_trace", "ldpc_ctx_last_kernel_ms", "ldpc_ctx_kernel_info", "ldpc_ctx_redo_count",
-            "ldpc_ctx_row_sched_info",
+            "ldpc_ctx_row_sched_info", "ldpc_ctx_set_option", "ldpc_ctx_get_option", "ldpc_nb_ctx_set_option",
             "ldpc_gdbf_decode_batch", "ldpc_gdbf_sim_launch", "ldpc_gdbf_sim_batch", "ldpc_gdbf_kernel_info",
             "ldpc_nb_graph_create", "ldpc_nb_graph_load_alist", "ldpc_nb_graph_info", "ldpc_nb_graph_destroy",
             "ldpc_nb_ctx_create", "ldpc_nb_ctx_set_stream", "ldpc_nb_ctx_destroy", "ldpc_nb_ctx_read_counts",
@@ -323,6 +355,26 @@ class Context:
     def set_stream(self, stream_handle: Optional[int]):
         _check(lib().ldpc_ctx_set_stream(self._h, stream_handle))
 
+    def set_option(self, name, value):
+        """Override the kernel choice (ldpc_ctx_set_option): name from OPTIONS, value an int
+        or a symbolic value from OPTION_VALUES (e.g. set_option("rows64", "fast"))."""
+        _check(lib().ldpc_ctx_set_option(self._h, option_id(name), option_value(name, value)))
+
+    def get_option(self, name) -> int:
+        v = C.c_int()
+        _check(lib().ldpc_ctx_get_option(self._h, option_id(name), C.byref(v)))
+        return int(v.value)
+
+    def set_options(self, opts: Optional[dict]):
+        for k, v in (opts or {}).items():
+            self.set_option(k, v)
+
+    def reset_options(self):
+        """Every option back to 0, the library's own kernel choice."""
+        for k in OPTIONS.values():
+            if k not in (20, 21):   # the EMS options belong to the nb context
+                _check(lib().ldpc_ctx_set_option(self._h, k, 0))
+
     def synchronize(self):
         _check(lib().ldpc_ctx_synchronize(self._h))
 
@@ -415,10 +467,10 @@ class Context:
 
     def row_sched_info(self, cfg: DecoderConfig) -> dict:
         """Shape of the row kernel that decodes cfg (raises LdpcError UNSUPPORTED for other kernels)."""
-        info = np.zeros(8, dtype=np.int32)
+        info = np.zeros(10, dtype=np.int32)
         _check(lib().ldpc_ctx_row_sched_info(self._h, C.byref(cfg._c()), info.ctypes.data))
         keys = ("threads", "rows_per_thread", "slots_per_thread", "dc", "e_pad", "cw_per_block", "lds_bytes",
-                "blocks_per_cu")
+                "blocks_per_cu", "dc_low", "issued_check_edges")
         return {k: int(v) for k, v in zip(keys, info)}
 
     def kernel_info(self, cfg: DecoderConfig) -> dict:
@@ -525,6 +577,10 @@ class NbContext:
 
     def set_stream(self, stream_handle: Optional[int]):
         _check(lib().ldpc_nb_ctx_set_stream(self._h, stream_handle))
+
+    def set_option(self, name, value):
+        """EMS options (ems_threads, ems_swizzle) of ldpc_nb_ctx_set_option."""
+        _check(lib().ldpc_nb_ctx_set_option(self._h, option_id(name), option_value(name, value)))
 
     def decode(self, y, n0: float, cfg: EmsConfig, c=None, want_decisions: bool = True):
         """Decode y[batch, N*m] float32 (numpy or torch, host or device). Returns (d [batch,N] uint8, frames, NbCounts)."""

@@ -38,6 +38,7 @@ class PointResult:
     rounds: int = 0
     frames_decoded: int = 0             # frames decoded over all ranks, incl. those past the stop
     hist: Optional[np.ndarray] = None   # error_weight_hist (:173), exact-stop frames only
+    collectives: dict = field(default_factory=dict)   # backend and calls of the collective layer
 
     @property
     def ber(self) -> float:
@@ -89,12 +90,16 @@ def exact_cut(prev: np.ndarray, frames: np.ndarray, T: int, min_bit_err=200, min
 
 
 class _Comm:
-    """Minimal collective layer: torch.distributed if initialised, else local."""
+    """Minimal collective layer: torch.distributed if initialised, else local. With a
+    process group the collectives always run, at world size 1 too (a one-rank RCCL
+    communicator under torchrun --nproc-per-node 1), so the path an 8-GPU run takes
+    is the path a one-GPU run executes."""
 
     def __init__(self, device=None):
         self.dist = None
         self.rank, self.world = 0, 1
         self.device = device
+        self.calls = {"allreduce": 0, "allgather": 0}
         try:
             import torch.distributed as dist
             if dist.is_available() and dist.is_initialized():
@@ -111,16 +116,18 @@ class _Comm:
         return t
 
     def allreduce_sum(self, arr: np.ndarray) -> np.ndarray:
-        if self.dist is None or self.world == 1:
+        if self.dist is None:
             return arr
+        self.calls["allreduce"] += 1
         t = self._tensor(arr)
         self.dist.all_reduce(t)
         return t.cpu().numpy()
 
     def allgather(self, arr: np.ndarray) -> np.ndarray:
         """Concatenate equal-shaped int arrays from all ranks, in rank order."""
-        if self.dist is None or self.world == 1:
+        if self.dist is None:
             return arr
+        self.calls["allgather"] += 1
         t = self._tensor(arr)
         out = [t.clone() for _ in range(self.world)]
         self.dist.all_gather(out, t)
@@ -270,6 +277,7 @@ def simulate_point(run_batch: Callable[[int, int], np.ndarray], N: int, T: int, 
     res.rounds = rounds0 + rnd
     res.frames_decoded = decoded
     res.hist = hist
+    res.collectives = {"backend": comm.dist.get_backend() if comm.dist else None, "world": comm.world, **comm.calls}
     return res
 
 

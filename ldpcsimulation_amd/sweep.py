@@ -127,7 +127,10 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     device = local if world > 1 and not a.share_device else 0
-    if world > 1:
+    # under torchrun (WORLD_SIZE set) a process group always exists, one rank included:
+    # the counters then go through the collective backend exactly as at 8 ranks
+    distributed = "WORLD_SIZE" in os.environ
+    if distributed:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(device)
@@ -141,7 +144,7 @@ def main(argv=None) -> int:
             raise checkpoint.CheckpointMismatch(f"--seed {a.seed} != the checkpoint's seed {ck.seed}")
         a.seed = ck.seed          # every rank read the same file
     seed = a.seed if a.seed is not None else int(time.time())
-    if world > 1 and a.seed is None:
+    if distributed and a.seed is None:
         # every rank must key its noise with rank 0's seed (ranks may start in different seconds)
         import torch
         import torch.distributed as dist
@@ -200,10 +203,11 @@ def main(argv=None) -> int:
             "mbit_s": ran * g.N / dt / 1e6 if dt > 0 else None,
             "n_gpus": world, "wilson95": sim.wilson_interval(c["frame_err"], c["frames"]),
             "precision": a.precision, "schedule": a.schedule, "variant": a.variant,
-            "kernel": ctx.kernel_info(cfg)["kernel"], "rounds": res.rounds, "frames_decoded": res.frames_decoded}
+            "kernel": ctx.kernel_info(cfg)["kernel"], "rounds": res.rounds, "frames_decoded": res.frames_decoded,
+            "collectives": res.collectives}
 
     _run_points(a, ck, rank, g.N, run_point)
-    if world > 1:
+    if distributed:
         import torch.distributed as dist
         dist.destroy_process_group()
     return 0
@@ -235,8 +239,8 @@ def _ems_sweep(a, seed, world, rank, device, ck=None) -> int:
             "precision": "f32", "rounds": res.rounds, "frames_decoded": res.frames_decoded}
 
     _run_points(a, ck, rank, bits, run_point)
-    if world > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     return 0
 

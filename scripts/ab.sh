@@ -2,9 +2,11 @@
 # One parametrised A/B driver for every kernel experiment (it replaces round 3's 35
 # one-off scripts/r03_probe*.sh; their arms and results are in profiles/ab_table_r03.md).
 #
-# Arms are whole environment settings, one quoted "VAR=v VAR2=w" string each (an empty
-# string is the default build); variant libraries are selected with LDPC_LIB=<name>
-# (lib/variants/libldpc_hip_<name>.so). Build them on the CPU side first:
+# Arms are extra arguments of the timed program, one quoted string each (an empty string
+# is the product library with its own kernel choice): "--lib ab/libldpc_hip_<name>.so"
+# loads a variant build, "--option rows64=fast" sets a kernel-choice option of the
+# context (ldpc_ctx_set_option; the library reads no environment). Build variants on
+# the CPU side first (and `make clean-ab` afterwards, so they stop travelling):
 #
 #   scripts/ab.sh build NAME MAKE_TARGET "VFLAGS"        e.g. build p4 ppvariant "-DLDPC_PP_PRIO=4"
 #
@@ -23,13 +25,13 @@ O=gpurun_out/ab; mkdir -p $O
 
 if [ "$mode" = build ]; then
   make "$2" NAME="$1" VFLAGS="$3" > /tmp/ab_build_$1.log 2>&1 || { tail -5 /tmp/ab_build_$1.log; exit 1; }
-  echo "built lib/variants/libldpc_hip_$1.so"
+  echo "built ab/libldpc_hip_$1.so"
   exit 0
 fi
 
 if [ "$mode" = check ]; then
   for arm in "$@"; do
-    env $arm timeout -k 10 400 python -u scripts/pp_check.py > $O/check.log 2>&1 || { echo "[$arm] parity FAILED"; tail -5 $O/check.log; exit 1; }
+    timeout -k 10 400 python -u scripts/pp_check.py $arm > $O/check.log 2>&1 || { echo "[$arm] parity FAILED"; tail -5 $O/check.log; exit 1; }
     echo "[$arm] $(tail -1 $O/check.log)"
   done
   exit 0
@@ -49,16 +51,16 @@ for r in $(seq 1 "$ROUNDS"); do
     out=$O/$mode-arm$i-$r
     case $mode in
       bench)
-        env $arm timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $out.json 2> $out.err || { echo "fail [$arm]"; tail -3 $out.err; exit 1; }
+        timeout -k 10 300 python bench.py --no-cpu-baseline $arm "$@" > $out.json 2> $out.err || { echo "fail [$arm]"; tail -3 $out.err; exit 1; }
         tail -1 $out.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('[$arm]', round(d['value'],1), 'Mbit/s', round(d['ms_per_step'],3), 'ms', d['kernel_info']['kernel'], 'ferr', d['fer']['frame_err'])" ;;
       ems)
-        env $arm timeout -k 10 300 python scripts/bench_ems.py "$@" > $out.json 2> $out.err || { echo "fail [$arm]"; tail -3 $out.err; exit 1; }
+        timeout -k 10 300 python scripts/bench_ems.py $arm "$@" > $out.json 2> $out.err || { echo "fail [$arm]"; tail -3 $out.err; exit 1; }
         python -c "
 import json
 for l in open('$out.json'):
     d=json.loads(l); print('[$arm]', d['ebn0_db'], 'dB', round(d['kernel_ms'],3), 'ms', round(d['coded_mbit_s_kernel']), 'Mbit/s', d.get('kernel'), 'fer', d['fer'])" ;;
       code)
-        env $arm timeout -k 10 300 python scripts/time_code.py "$CODE" "$@" > $out.log 2>&1 || { echo "fail [$arm]"; tail -3 $out.log; exit 1; }
+        timeout -k 10 300 python scripts/time_code.py "$CODE" $arm "$@" > $out.log 2>&1 || { echo "fail [$arm]"; tail -3 $out.log; exit 1; }
         echo "[$arm] $(tail -1 $out.log)" ;;
       *) echo "unknown mode $mode"; exit 2 ;;
     esac

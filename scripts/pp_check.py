@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Ping-pong kernel (rows_pp.hip) against the other row kernels and the oracle on the
 bench code: same Philox channel, decisions/per-frame results/counters equal.
-fp64: pp vs k_rows_fast (LDPC_ROWS=fast); fp32 pairs: pp (LDPC_ROWS32=pp) vs the row
-kernel (k_decode_rows, the fp32 default) and the pair instance of k_rows_fast."""
+fp64: pp vs k_rows_fast (option rows64 = fast); fp32 pairs: pp vs the row kernel
+(rows32 = rows) and the pair instance of k_rows_fast (rows32 = fast).
+usage: pp_check.py [--lib ab/libldpc_hip_NAME.so]   (a variant build under A/B)"""
 import os
 import sys
 
@@ -15,6 +16,9 @@ import torch  # noqa: E402,F401  (one HIP runtime: torch first)
 from ldpcsimulation_amd import codes, native  # noqa: E402
 from oracle import oracle as O  # noqa: E402
 
+if len(sys.argv) > 2 and sys.argv[1] == "--lib":
+    native.use_library(os.path.abspath(sys.argv[2]))
+
 path = codes.ensure_80211n_1944()
 g = native.Graph.from_alist(path)
 ctx = native.Context(g, 0, 4096)
@@ -25,13 +29,12 @@ CASES = ((2048, 50, dict(variant=native.NMS, alpha=1.25)), (257, 7, dict(variant
 for prec in (native.F64, native.F32):
     for batch, T, vk in CASES:
         cfg = native.DecoderConfig(T=T, precision=prec, **vk)
-        arms = {"f64": [("fast", dict(LDPC_ROWS="fast")), ("pp", {})],
-                "f32": [("rows", {}), ("fast32", dict(LDPC_ROWS32="fast")), ("pp", dict(LDPC_ROWS32="pp"))]}
+        arms = {"f64": [("fast", dict(rows64="fast")), ("pp", {})],
+                "f32": [("rows", dict(rows32="rows")), ("fast32", dict(rows32="fast")), ("pp", {})]}
         res = {}
-        for name, env in arms["f64" if prec == native.F64 else "f32"]:
-            for k in ("LDPC_ROWS", "LDPC_ROWS32"):
-                os.environ.pop(k, None)
-            os.environ.update(env)
+        for name, opts in arms["f64" if prec == native.F64 else "f32"]:
+            ctx.reset_options()
+            ctx.set_options(opts)
             kern = ctx.kernel_info(cfg)["kernel"]
             res[name] = (kern, ctx.sim_trace(1.5, 0.5, cfg, seed=99, stream_id=3, first_cw=0, batch=batch),
                          ctx.redo_count())

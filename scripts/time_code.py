@@ -24,11 +24,19 @@ def main():
     ap.add_argument("--prec", default="f32")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--schedule", choices=["flooding", "layered"], default="flooding")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="a kernel-choice option of the context (native.OPTIONS), A/B only")
+    ap.add_argument("--lib", default=None, help="another build of the decoder library (A/B only)")
     ap.add_argument("--decoder", choices=["minsum", "gdbf"], default="minsum",
                     help="gdbf: SMNGDBF (theta -0.6, eta 0.75, lambda 0.99, w 0.8, window 16, Ymax 2.5)")
     a = ap.parse_args()
+    if a.lib:
+        native.use_library(os.path.abspath(a.lib))
     g = native.Graph.from_alist(a.alist)
     ctx = native.Context(g, 0, a.batch)
+    for o in a.option:
+        k, _, v = o.partition("=")
+        ctx.set_option(k, int(v) if v.isdigit() else v)
     v = {"ms": dict(variant=native.MS), "nms": dict(variant=native.NMS, alpha=1.25),
          "oms": dict(variant=native.OMS, delta=0.15), "bp": dict(variant=native.BP)}[a.variant]
     cfg = native.DecoderConfig(T=a.T, precision=native.F32 if a.prec == "f32" else native.F64,

@@ -56,6 +56,7 @@ def gpu_ctx_factory():
         if key not in cache:
             g = native.Graph.from_alist(code_path(code) if not os.path.isabs(code) else code)
             cache[key] = native.Context(g, 0, max_batch)
+        cache[key].reset_options()   # kernel-choice options a previous test set stay with that test
         return cache[key]
 
     return make

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     L = native.lib()
-    assert L.ldpc_abi_version() == native.ABI_VERSION == 9
+    assert L.ldpc_abi_version() == native.ABI_VERSION == 10
     with pytest.raises(native.LdpcError) as e:
         native.Graph.from_alist("/nonexistent/file.alist")
     assert e.value.code == -5
@@ -98,3 +98,63 @@ def test_shipped_library_holds_only_the_kept_ping_pong_kernel():
     with open(native.LIB_PATH, "rb") as f:
         blob = f.read()
     assert b"LDPC_PP_MODE" not in blob and b"pp_wait" not in blob
+
+
+# Every environment variable that chose a kernel before ABI 10.
+FORMER_KNOBS = ["LDPC_ROWS", "LDPC_ROWS32", "LDPC_PP_ROWS", "LDPC_KERNEL", "LDPC_FORCE_GLOBAL", "LDPC_FLOOD_MODE",
+                "LDPC_FLOOD_MSG", "LDPC_FLOOD_SPS_CHECK", "LDPC_FLOOD_SPS_BIT", "LDPC_FLOOD_RESIDENT",
+                "LDPC_FLOOD_STREAMS", "LDPC_FLOOD_BPC", "LDPC_LAYERED_BPC", "LDPC_LAYERED_LDS_POS",
+                "LDPC_LAYERED_R64", "LDPC_LAYERED_THREADS", "LDPC_BLOCKS_PER_CU", "LDPC_FAST_BPC", "LDPC_RPT",
+                "LDPC_BP_KERNEL", "LDPC_GDBF_KERNEL", "LDPC_EMS_THREADS", "LDPC_EMS_SWIZZLE", "LDPC_LIB"]
+KNOB_VALUES = {"LDPC_ROWS": "old", "LDPC_ROWS32": "rows", "LDPC_PP_ROWS": "plain", "LDPC_KERNEL": "global",
+               "LDPC_FORCE_GLOBAL": "1", "LDPC_FLOOD_MODE": "persistent", "LDPC_FLOOD_MSG": "c2v",
+               "LDPC_BP_KERNEL": "generic", "LDPC_GDBF_KERNEL": "generic", "LDPC_LIB": "ppst"}
+
+
+def test_shipped_library_reads_no_environment():
+    """Kernel selection is an ABI option (ldpc_ctx_set_option), never the environment:
+    the product library imports no getenv/secure_getenv and holds none of the former
+    knobs' names, so no variable can reroute it (the reference fixes its algorithm per
+    binary at build time, C_implementations/Makefile:58-65)."""
+    import subprocess
+    und = subprocess.run(["nm", "-D", "--undefined-only", native.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", und), und
+    with open(native.LIB_PATH, "rb") as f:
+        blob = f.read()
+    for k in FORMER_KNOBS:
+        assert k.encode() not in blob, k
+    src = open(os.path.join(ROOT, "ldpcsimulation_amd", "native.py")).read()
+    assert "LDPC_LIB" not in src and "os.environ" not in src and "getenv" not in src
+
+
+def test_python_host_ignores_former_knobs(monkeypatch):
+    """With every former knob set, the Python host still loads the product library and
+    names the same defaults (the options are per-context ABI calls)."""
+    import importlib
+    for k in FORMER_KNOBS:
+        monkeypatch.setenv(k, KNOB_VALUES.get(k, "1"))
+    mod = importlib.reload(native)
+    try:
+        assert mod.LIB_PATH.endswith(os.path.join("lib", "libldpc_hip.so"))
+        assert mod.option_id("rows64") == 1 and mod.option_value("rows64", "pp") == 0
+    finally:
+        monkeypatch.undo()
+        importlib.reload(native)
+
+
+def test_option_enum_matches_header():
+    """native.OPTIONS mirrors include/ldpc_hip.h's ldpc_option enum."""
+    txt = open(os.path.join(ROOT, "include", "ldpc_hip.h")).read()
+    enum = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"LDPC_OPT_([A-Z0-9_]+)\s*=\s*(\d+)", txt)}
+    assert enum == native.OPTIONS
+    assert int(re.search(r"#define LDPC_OPT_COUNT (\d+)", txt).group(1)) == max(enum.values()) + 1
+
+
+def test_set_option_validates_without_a_device():
+    """Option validation happens before any device call: a NULL context is refused."""
+    L = native.lib()
+    assert L.ldpc_ctx_set_option(None, 1, 0) == -1
+    assert L.ldpc_nb_ctx_set_option(None, 20, 512) == -1
+    v = C.c_int(7)
+    assert L.ldpc_ctx_get_option(None, 1, C.byref(v)) == -1

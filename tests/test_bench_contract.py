@@ -68,14 +68,23 @@ def test_gpus_without_torchrun_spawns_ranks(monkeypatch):
 
 
 def test_lds_model_of_the_n1944_row_schedule():
-    """The LDS roofline model for the N=1944 schedule: 1024 row slots x 8,
-    e_pad 7232, 512 x 4 bit slots -> 1442 LDS-array cycles per group-iteration."""
+    """The LDS roofline models for the N=1944 code (E = 6966): the headline
+    `frac` is the algorithmic one -- E gathers + E scatters + E bit reads + N app writes,
+    no padding: 1270.7 LDS-array cycles per codeword-iteration; the
+    companions are the kernel's issued slots (768 x 7 + 256 x 8 check edges with the
+    degree-aware slots, as the library reports them: 1346) and the padded rows-2..4
+    model (1024 row slots x 8, e_pad 7232, 512 x 4 bit slots: 1442)."""
     b = _bench()
     si = {"threads": 512, "rows_per_thread": 2, "slots_per_thread": 4, "dc": 8, "e_pad": 7232,
-          "cw_per_block": 1, "lds_bytes": 74576, "blocks_per_cu": 2}
-    m = b.lds_model(si, 1944)
-    assert m["by_phase"] == {"check_gather": 256, "check_scatter": 768, "bit_read": 226, "app_write": 192}
-    assert m["cycles_per_group_iter"] == 1442
+          "cw_per_block": 1, "lds_bytes": 148520, "blocks_per_cu": 1, "dc_low": 7,
+          "issued_check_edges": 768 * 7 + 256 * 8}
+    m = b.lds_model(si, 6966, 1944)
+    assert m["by_phase"] == {"check_gather": 6966 / 32, "check_scatter": 6966 * 6 / 64, "bit_read": 6966 / 32,
+                             "app_write": 1944 * 6 / 64}
+    assert abs(m["cycles_per_group_iter"] - 1270.6875) < 1e-9
+    alt = b.lds_models_alt(si)
+    assert alt["issued"]["cycles_per_group_iter"] == 116 * 8 + 226 + 192 == 1346
+    assert alt["padded"]["cycles_per_group_iter"] == 1442 and alt["issued"]["degree_split"]
 
 
 def test_cpu_share_is_capped(monkeypatch):

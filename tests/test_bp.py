@@ -192,7 +192,7 @@ def test_bp_rows_kernel_equals_generic_kernel(gpu_ctx_factory, monkeypatch, code
         return
     assert ctx.kernel_info(cfg)["kernel"] == "bp_rows"
     got = [ctx.sim_trace(e, 0.5, cfg, seed=17, stream_id=3, first_cw=64, batch=1024) for e in (1.0, 2.0)]
-    monkeypatch.setenv("LDPC_BP_KERNEL", "generic")
+    ctx.set_option("bp_kernel", "generic")
     assert ctx.kernel_info(cfg)["kernel"] != "bp_rows"
     for e, (y, d, fr, cnt) in zip((1.0, 2.0), got):
         y2, d2, fr2, cnt2 = ctx.sim_trace(e, 0.5, cfg, seed=17, stream_id=3, first_cw=64, batch=1024)

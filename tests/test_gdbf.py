@@ -229,7 +229,7 @@ def test_gdbf_rows_kernel_equals_generic_kernel(gpu_ctx_factory, monkeypatch, co
     for snr in (2.0, 3.0):
         fr, cnt = ctx.gdbf_sim_batch(snr, 0.5, cfg, seed=31, stream_id=2, first_cw=100, batch=2048)
         res[snr] = (fr, cnt.as_dict())
-    monkeypatch.setenv("LDPC_GDBF_KERNEL", "generic")
+    ctx.set_option("gdbf_kernel", "generic")
     assert ctx.gdbf_kernel_info(cfg)["kernel"] != "gdbf_rows"
     for snr in (2.0, 3.0):
         fr, cnt = ctx.gdbf_sim_batch(snr, 0.5, cfg, seed=31, stream_id=2, first_cw=100, batch=2048)

@@ -165,12 +165,9 @@ def test_all_kernels_bit_identical(monkeypatch, code):
     g = native.Graph.from_alist(code_path(code))
     ctxs = {}
     for k in ("default", "lds", "flood", "global"):
-        if k == "default":
-            monkeypatch.delenv("LDPC_KERNEL", raising=False)
-        else:
-            monkeypatch.setenv("LDPC_KERNEL", k)
         ctxs[k] = native.Context(g, 0, 300)
-    monkeypatch.delenv("LDPC_KERNEL", raising=False)
+        if k != "default":
+            ctxs[k].set_option("kernel", k)
     cfgs = [native.DecoderConfig(variant=native.OMS, delta=0.1, T=15, quantize=True, ymax=1.5, qbits=5),
             native.DecoderConfig(variant=native.NMS, alpha=1.25, T=15),
             native.DecoderConfig(variant=native.MS, T=15)]
@@ -187,17 +184,17 @@ def test_all_kernels_bit_identical(monkeypatch, code):
             f32_default = "rows_pp" if pp_code and cfg.variant != native.OMS else "rows"
             assert names["default"] == (f64_default if prec == native.F64 else f32_default)
         outs = {k: c.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300) for k, c in ctxs.items()}
-        monkeypatch.setenv("LDPC_ROWS", "fast")   # fp64: the one-codeword fast kernel where pp is the default
-        outs["rows_fast"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
-        monkeypatch.delenv("LDPC_ROWS", raising=False)
-        monkeypatch.setenv("LDPC_ROWS", "old")   # the previous row kernel (exact + fast loops in one)
-        outs["rows_old"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
-        monkeypatch.delenv("LDPC_ROWS", raising=False)
-        monkeypatch.setenv("LDPC_ROWS32", "fast")   # fp32: the pair instance of rows_fast (opt-in)
-        outs["rows_fast32"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
-        monkeypatch.setenv("LDPC_ROWS32", "rows")   # fp32: the row kernel
-        outs["rows32"] = ctxs["default"].sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
-        monkeypatch.delenv("LDPC_ROWS32", raising=False)
+        cd = ctxs["default"]
+        cd.set_option("rows64", "fast")   # fp64: the one-codeword fast kernel where pp is the default
+        outs["rows_fast"] = cd.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
+        cd.set_option("rows64", "rows")   # the previous row kernel (exact + fast loops in one)
+        outs["rows_old"] = cd.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
+        cd.set_option("rows64", "pp")
+        cd.set_option("rows32", "fast")   # fp32: the pair instance of rows_fast (opt-in)
+        outs["rows_fast32"] = cd.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
+        cd.set_option("rows32", "rows")   # fp32: the row kernel
+        outs["rows32"] = cd.sim_trace(2.0, 0.5, cfg, 9, 0, 0, 300)
+        cd.set_option("rows32", "pp")
         ref = outs["global"]
         for k, o in outs.items():
             for a, b in zip(o[:3], ref[:3]):
@@ -360,8 +357,8 @@ def test_flood_heavy_column_vs_oracle(tmp_path, monkeypatch, prec):
         rows[j] = sorted(set(rows[j]) | {0})
     path = str(tmp_path / "heavy_col.alist")
     codes.write_alist(codes.ParityCheck.from_rows(N, rows), path)
-    monkeypatch.setenv("LDPC_KERNEL", "flood")
     ctx = native.Context(native.Graph.from_alist(path), 0, 64)
+    ctx.set_option("kernel", "flood")
     f32 = prec == "f32"
     y = _glibc_frames(N, 16, 3.0, 0.5, seed=41)
     if f32:

@@ -133,9 +133,8 @@ def test_layered_decisions_bit_exact_vs_oracle(gpu_ctx_factory, code, vname, pre
 def test_layered_lds_and_global_identical(monkeypatch, code):
     native = _native()
     g = native.Graph.from_alist(code_path(code))
-    monkeypatch.setenv("LDPC_KERNEL", "global")
     cg = native.Context(g, 0, 200)
-    monkeypatch.delenv("LDPC_KERNEL", raising=False)
+    cg.set_option("kernel", "global")
     cl = native.Context(g, 0, 200)
     for prec in (native.F32, native.F64):
         cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=12, precision=prec, schedule=native.LAYERED)

@@ -80,29 +80,29 @@ def _glibc_frames(N, nframes, ebn0, R, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("code", ["80211n_1944_r12.alist", "PEGReg504x1008.alist"])
-def test_fast_kernel_is_the_f64_row_kernel(gpu_ctx_factory, monkeypatch, code):
+def test_fast_kernel_is_the_f64_row_kernel(gpu_ctx_factory, code):
     """fp64 row graphs take a fast-path kernel: the ping-pong kernel (rows_pp.hip) for
     the 802.11n code (M = 972: 512 threads x 2 rows), k_rows_fast otherwise or with
-    LDPC_ROWS=fast (the kernel the tests of this file exercise)."""
+    option rows64 = fast (the kernel the tests of this file exercise)."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(code)
     cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=5, precision=native.F64)
     assert ctx.kernel_info(cfg)["kernel"] == ("rows_pp" if code == "80211n_1944_r12.alist" else "rows_fast")
-    monkeypatch.setenv("LDPC_ROWS", "fast")
+    ctx.set_option("rows64", "fast")
     assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
     cfg.precision = native.F32                       # fp32: pairs on the ping-pong kernel where it fits
     assert ctx.kernel_info(cfg)["kernel"] == ("rows_pp" if code == "80211n_1944_r12.alist" else "rows")
-    monkeypatch.setenv("LDPC_ROWS32", "rows")
+    ctx.set_option("rows32", "rows")
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
 
 
 @pytest.mark.gpu
-def test_f32_pair_fast_kernel_opt_in(gpu_ctx_factory, monkeypatch):
-    """LDPC_ROWS32=fast selects the fp32 pair instance of rows_fast for MS and
+def test_f32_pair_fast_kernel_opt_in(gpu_ctx_factory):
+    """Option rows32 = fast selects the fp32 pair instance of rows_fast for MS and
     verified-reciprocal NMS; OMS keeps the row kernel."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory("80211n_1944_r12.alist")
-    monkeypatch.setenv("LDPC_ROWS32", "fast")
+    ctx.set_option("rows32", "fast")
     for v, want in ((native.MS, "rows_fast"), (native.NMS, "rows_fast"), (native.OMS, "rows")):
         cfg = native.DecoderConfig(variant=v, alpha=1.25, delta=0.1, T=5, precision=native.F32)
         assert ctx.kernel_info(cfg)["kernel"] == want
@@ -113,15 +113,15 @@ def test_f32_pair_fast_kernel_opt_in(gpu_ctx_factory, monkeypatch):
 @pytest.mark.parametrize("vname,v", [("ms", dict(variant=0)), ("nms", dict(variant=1, alpha=1.25)),
                                      ("nms_ieee", dict(variant=1, alpha=1.1)),
                                      ("oms", dict(variant=2, delta=0.15))])
-def test_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, code, vname, v):
+def test_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, code, vname, v):
     """Frames built to break the fast premise (|y| >= 2^1000, minima below 2^-960, inf,
     NaN, values growing past 2^1000 mid-decode) are re-decoded on the exact path:
     decisions, error weights and counters equal the fp64 oracle's for every frame,
     and the re-decode list holds exactly the frames that broke it. (k_rows_fast; the
     ping-pong kernel's twin is tests/test_rows_pp.py.)"""
     from ldpcsimulation_amd import native
-    monkeypatch.setenv("LDPC_ROWS", "fast")
     ctx = gpu_ctx_factory(code)
+    ctx.set_option("rows64", "fast")
     N = ctx.graph.N
     y = _glibc_frames(N, 16, 1.5, 0.5, seed=4242)
     y[1] *= 1e305                     # input premise: |yq| >= 2^1000
@@ -150,14 +150,14 @@ def test_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, code
 @pytest.mark.gpu
 @pytest.mark.parametrize("code", ["80211n_1944_r12.alist", "PEGReg504x1008.alist"])
 @pytest.mark.parametrize("vname,v", [("ms", dict(variant=0)), ("nms", dict(variant=1, alpha=1.25))])
-def test_f32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, code, vname, v):
+def test_f32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, code, vname, v):
     """fp32: frames that break the fast premise (|yq| >= 1e30, inf, NaN, values growing
-    past 1e30 mid-decode) -- the pair instance of rows_fast (LDPC_ROWS32=fast) re-decodes
+    past 1e30 mid-decode) -- the pair instance of rows_fast (option rows32 = fast) re-decodes
     them on the exact path, the row kernel hands them over to its exact loop; both give
     the fp32 oracle's decisions and counters."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(code)
-    monkeypatch.setenv("LDPC_ROWS32", "fast")
+    ctx.set_option("rows32", "fast")
     N = ctx.graph.N
     y = _glibc_frames(N, 16, 1.5, 0.5, seed=4243).astype(np.float32)
     y[1] *= np.float32(1e31)          # input premise: |yq| >= 1e30
@@ -181,10 +181,10 @@ def test_f32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, 
         assert cnt.frames == len(y) and cnt.bit_err == int(w.sum()) and cnt.iters == T * len(y)
         # pairs (0,1), (2,3), (4,5) break (frame 5 shares frame 4's pair); a pair is re-decoded whole
         assert redo == 6, redo
-        monkeypatch.setenv("LDPC_ROWS32", "rows")
+        ctx.set_option("rows32", "rows")
         assert ctx.kernel_info(cfg)["kernel"] == "rows"
         d_old, fr_old, cnt_old = ctx.decode(y, cfg)
-        monkeypatch.setenv("LDPC_ROWS32", "fast")
+        ctx.set_option("rows32", "fast")
         assert np.array_equal(d_old, d) and np.array_equal(fr_old, fr) and cnt_old.bit_err == cnt.bit_err
 
 
@@ -192,14 +192,14 @@ def test_f32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, 
 @pytest.mark.parametrize("ebn0", [1.5, 1.75])
 @pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0))])
 @pytest.mark.parametrize("kernel", ["pp", "fast"])
-def test_f64_headline_config_bit_exact(gpu_ctx_factory, monkeypatch, kernel, ebn0, vname, v):
+def test_f64_headline_config_bit_exact(gpu_ctx_factory, kernel, ebn0, vname, v):
     """The bench configuration in fp64 (802.11n N=1944, T=50, on-device Philox channel):
     2048 codewords per point, decisions identical to the fp64 oracle on the same y,
     and no codeword needed the exact path -- for the bench's kernel (the ping-pong
     kernel, rows_pp.hip) and for k_rows_fast."""
     from ldpcsimulation_amd import native
-    monkeypatch.setenv("LDPC_ROWS", kernel)
     ctx = gpu_ctx_factory("80211n_1944_r12.alist")
+    ctx.set_option("rows64", kernel)
     cfg = native.DecoderConfig(T=50, precision=native.F64, **v)
     assert ctx.kernel_info(cfg)["kernel"] == "rows_" + kernel
     y, d, fr, cnt = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261016, stream_id=1, first_cw=0, batch=2048)
@@ -214,25 +214,24 @@ def test_f64_headline_config_bit_exact(gpu_ctx_factory, monkeypatch, kernel, ebn
 @pytest.mark.gpu
 @pytest.mark.parametrize("ebn0", [1.5, 1.75])
 @pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0))])
-def test_f32_bench_kernel_bit_exact_at_T50(gpu_ctx_factory, monkeypatch, ebn0, vname, v):
+def test_f32_bench_kernel_bit_exact_at_T50(gpu_ctx_factory, ebn0, vname, v):
     """The fp32 bench kernel (k_decode_rows<float, PHILOX, 2, 8, 4, 2>: fast check node,
     reciprocal NMS, fast->exact hand-over) at the bench's T=50 on 2048 codewords per
     point: decisions identical to the fp32 oracle on the same y, to
-    the opt-in pair instance of rows_fast (LDPC_ROWS32=fast) and to the fp32 default,
+    the opt-in pair instance of rows_fast (option rows32 = fast) and to the fp32 default,
     the ping-pong kernel's float2 slots (rows_pp.hip)."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory("80211n_1944_r12.alist")
     cfg = native.DecoderConfig(T=50, precision=native.F32, **v)
-    monkeypatch.setenv("LDPC_ROWS32", "rows")
+    ctx.set_option("rows32", "rows")
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
     y, d, fr, cnt = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261017, stream_id=2, first_cw=0, batch=2048)
     for k32, name in (("fast", "rows_fast"), ("pp", "rows_pp")):   # the opt-in pair kernel, the fp32 default
-        monkeypatch.setenv("LDPC_ROWS32", k32)
+        ctx.set_option("rows32", k32)
         assert ctx.kernel_info(cfg)["kernel"] == name
         y_f, d_f, fr_f, _ = ctx.sim_trace(ebn0, 0.5, cfg, seed=20261017, stream_id=2, first_cw=0, batch=2048)
         assert ctx.redo_count() == 0
         assert np.array_equal(y_f, y) and np.array_equal(d_f, d) and np.array_equal(fr_f, fr), k32
-    monkeypatch.delenv("LDPC_ROWS32")
     want = O.Alist(code_path("80211n_1944_r12.alist")).decode(y, 50, O.Cfg(**v), workers=16)
     assert int((d != want).sum()) == 0
     assert np.array_equal(fr["bit_err"], (want != 1).sum(axis=1))

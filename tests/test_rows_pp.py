@@ -20,20 +20,20 @@ from oracle import oracle as O
 CODE = "80211n_1944_r12.alist"
 
 
-def _kernel(monkeypatch, name):
-    monkeypatch.setenv("LDPC_ROWS", name)
+def _kernel(ctx, name):
+    ctx.set_option("rows64", name)
 
 
 @pytest.mark.gpu
-def test_pp_kernel_selected_for_the_bench_code(gpu_ctx_factory, monkeypatch):
+def test_pp_kernel_selected_for_the_bench_code(gpu_ctx_factory):
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(CODE)
     cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50, precision=native.F64)
-    _kernel(monkeypatch, "pp")
+    _kernel(ctx, "pp")
     assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
-    _kernel(monkeypatch, "fast")
+    _kernel(ctx, "fast")
     assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
-    monkeypatch.delenv("LDPC_ROWS")
+    ctx.reset_options()
     info = ctx.kernel_info(cfg)
     assert info["kernel"] == "rows_pp"      # the default
     # two slots of app[N+3] + c2v[e_pad+64] in one block per CU
@@ -53,13 +53,13 @@ def test_pp_kernel_selected_for_the_bench_code(gpu_ctx_factory, monkeypatch):
     (3, 0, dict(variant=1, alpha=1.25)),         # no iteration: decisions of the channel
     (1, 13, dict(variant=0)),                    # one codeword, empty partner slot
 ])
-def test_pp_equals_rows_fast_and_oracle(gpu_ctx_factory, monkeypatch, batch, T, v):
+def test_pp_equals_rows_fast_and_oracle(gpu_ctx_factory, batch, T, v):
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(CODE)
     cfg = native.DecoderConfig(T=T, precision=native.F64, **v)
-    _kernel(monkeypatch, "fast")
+    _kernel(ctx, "fast")
     y0, d0, f0, c0 = ctx.sim_trace(1.5, 0.5, cfg, seed=77, stream_id=5, first_cw=123, batch=batch)
-    _kernel(monkeypatch, "pp")
+    _kernel(ctx, "pp")
     y1, d1, f1, c1 = ctx.sim_trace(1.5, 0.5, cfg, seed=77, stream_id=5, first_cw=123, batch=batch)
     assert ctx.redo_count() == 0
     assert np.array_equal(y0, y1)
@@ -82,14 +82,14 @@ def _glibc_frames(N, nframes, ebn0, R, seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0)),
                                      ("oms", dict(variant=2, delta=0.15))])
-def test_pp_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, vname, v):
+def test_pp_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, vname, v):
     """Frames 1-5 break the fast premise (|y| >= 2^1000, tiny minima, inf, NaN, growth
     past 2^1000); their pair partners (0, and the unbroken frames 6-9 sharing no pair
     with them) decode normally. Everything equals the fp64 oracle; the re-decode list
     holds the broken codewords only (not whole pairs)."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(CODE)
-    _kernel(monkeypatch, "pp")
+    _kernel(ctx, "pp")
     N = ctx.graph.N
     y = _glibc_frames(N, 12, 1.5, 0.5, seed=4244)
     y[1] *= 1e305
@@ -139,7 +139,7 @@ def _random_code(tmp_path, name, N, M, row_deg, seed):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", ["bench", "all_deg8", "low_deg"])
-def test_pp_row_slot_layouts_equal_each_other_and_oracle(tmp_path, monkeypatch, shape):
+def test_pp_row_slot_layouts_equal_each_other_and_oracle(tmp_path, shape):
     """The degree-aware row slots (graph.h pp_row_slots: the younger check wave of each
     SIMD runs two 7-edge check nodes) and the plain slots give the same values: rows of
     a flooding iteration are independent (decodeMinSum.cpp:410-450), so moving them
@@ -160,12 +160,12 @@ def test_pp_row_slot_layouts_equal_each_other_and_oracle(tmp_path, monkeypatch, 
     cfg = native.DecoderConfig(variant=1, alpha=1.25, T=30, precision=native.F64)
     outs = {}
     for slots in ("plain", "split"):
-        monkeypatch.setenv("LDPC_PP_ROWS", slots)
+        ctx.set_option("pp_slots", slots)
         assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
         outs[slots] = ctx.sim_trace(2.5, 0.5, cfg, seed=31, stream_id=2, first_cw=0, batch=515)
         assert ctx.redo_count() == 0
-    monkeypatch.delenv("LDPC_PP_ROWS")
-    _kernel(monkeypatch, "fast")
+    ctx.set_option("pp_slots", "split")
+    _kernel(ctx, "fast")
     outs["fast"] = ctx.sim_trace(2.5, 0.5, cfg, seed=31, stream_id=2, first_cw=0, batch=515)
     for k in ("split", "fast"):
         for a, b in zip(outs[k][:3], outs["plain"][:3]):
@@ -183,17 +183,17 @@ def test_pp_row_slot_layouts_equal_each_other_and_oracle(tmp_path, monkeypatch, 
     (2, 7, dict(variant=1, alpha=1.25)),         # one pair, the other slot empty
     (5, 0, dict(variant=0)),                     # no iteration
 ])
-def test_pp_fp32_pairs_equal_row_kernel_and_oracle(gpu_ctx_factory, monkeypatch, batch, T, v):
+def test_pp_fp32_pairs_equal_row_kernel_and_oracle(gpu_ctx_factory, batch, T, v):
     """fp32 pairs on the ping-pong kernel (the fp32 default: two float2 slots, four codewords
     per block step) give the fp32 row kernel's channel, decisions, per-frame results and
     counters, and the fp32 oracle's decisions (decodeMinSum.cpp:410-476 in float)."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(CODE)
     cfg = native.DecoderConfig(T=T, precision=native.F32, **v)
-    monkeypatch.setenv("LDPC_ROWS32", "rows")
+    ctx.set_option("rows32", "rows")
     assert ctx.kernel_info(cfg)["kernel"] == "rows"
     y0, d0, f0, c0 = ctx.sim_trace(1.5, 0.5, cfg, seed=78, stream_id=6, first_cw=321, batch=batch)
-    monkeypatch.delenv("LDPC_ROWS32")                 # the fp32 default
+    ctx.set_option("rows32", "pp")                    # the fp32 default
     assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
     y1, d1, f1, c1 = ctx.sim_trace(1.5, 0.5, cfg, seed=78, stream_id=6, first_cw=321, batch=batch)
     assert ctx.redo_count() == 0
@@ -206,13 +206,13 @@ def test_pp_fp32_pairs_equal_row_kernel_and_oracle(gpu_ctx_factory, monkeypatch,
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("vname,v", [("nms", dict(variant=1, alpha=1.25)), ("ms", dict(variant=0))])
-def test_pp_fp32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypatch, vname, v):
+def test_pp_fp32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, vname, v):
     """fp32 pairs: frames whose inputs or messages leave the fast premise (|y| >= 1e30,
     inf, NaN, growth past 1e30) hand their pair to the exact re-decode; every decision
     equals the fp32 oracle's and the other pair of the step is unaffected."""
     from ldpcsimulation_amd import native
     ctx = gpu_ctx_factory(CODE)
-    monkeypatch.setenv("LDPC_ROWS32", "pp")
+    ctx.set_option("rows32", "pp")
     N = ctx.graph.N
     y = _glibc_frames(N, 12, 1.5, 0.5, seed=4245).astype(np.float32)
     y[1] *= np.float32(1e31)
@@ -231,3 +231,30 @@ def test_pp_fp32_premise_breaks_are_redecoded_exactly(gpu_ctx_factory, monkeypat
         assert np.array_equal(fr["bit_err"], (want != 1).sum(axis=1))
         assert cnt.frames == len(y) and cnt.iters == T * len(y)
         assert ctx.redo_count() >= 4        # the pairs of frames 1, 3, 4 (and 9 once it grows)
+
+
+@pytest.mark.gpu
+def test_environment_cannot_reroute_the_product(monkeypatch):
+    """with every former kernel-choice variable set to a non-default
+    value, a fresh context still decodes the bench configuration on rows_pp (fp64) with
+    the degree-aware slots, and gives the same results as the same context after
+    ldpc_ctx_set_option has switched it to rows_fast and back."""
+    from test_abi import FORMER_KNOBS, KNOB_VALUES
+    from ldpcsimulation_amd import native
+    for k in FORMER_KNOBS:
+        monkeypatch.setenv(k, KNOB_VALUES.get(k, "1"))
+    ctx = native.Context(native.Graph.from_alist(code_path(CODE)), 0, 1024)
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50, precision=native.F64)
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
+    assert all(ctx.get_option(k) == 0 for k in native.OPTIONS if not k.startswith("ems"))
+    cfg32 = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50, precision=native.F32)
+    assert ctx.kernel_info(cfg32)["kernel"] == "rows_pp"
+    a = ctx.sim_trace(1.5, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=512)
+    ctx.set_option("rows64", "fast")
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_fast"
+    b = ctx.sim_trace(1.5, 0.5, cfg, seed=5, stream_id=0, first_cw=0, batch=512)
+    ctx.set_option("rows64", "pp")
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+    assert a[3].as_dict() == b[3].as_dict()

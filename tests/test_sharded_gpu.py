@@ -211,3 +211,57 @@ def test_sweep_checkpoint_resume(tmp_path):
     assert js[1]["resumed_from_frame"] == r1[2]["next_frame"] > 0
     assert run("--log", str(tmp_path / "c.txt"), "--checkpoint", str(ck)) == []
     assert not (tmp_path / "c.txt").exists()
+
+
+def _torchrun1(root, args, timeout=600):
+    """One rank under torchrun (WORLD_SIZE=1): the process group exists, so every counter
+    all-reduce and the cut round's all_gather go through the collective backend."""
+    return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                           "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args,
+                          cwd=root, env=dict(os.environ), capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.gpu
+def test_sweep_one_rank_rccl_equals_no_dist(tmp_path):
+    """the RCCL path executes on the MI355X. sweep.main under a one-rank
+    torchrun with --backend nccl (init_process_group("nccl", device_id=...), the int64
+    device all-reduce of every round, the device all_gather of the cut round where the
+    stop rule is crossed) gives the totals and the log line of a run without
+    torch.distributed -- the process-per-point model of
+    scripts/minsum_example_PEGReg504x1008.sh:23-27 and the stop rule of
+    decodeMinSum.cpp:189."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = [code_path(CODE), "--rate", "0.5", "--snr", "1.5", "-T", "50", "--variant", "nms", "--alpha", "1.25",
+            "--batch", "2048", "--seed", "4242", "--json"]
+    p = _torchrun1(root, ["-m", "ldpcsimulation_amd.sweep"] + args + ["--backend", "nccl",
+                                                                       "--log-file", str(tmp_path / "nccl.txt")])
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = [json.loads(l[l.index("{"):]) for l in p.stdout.splitlines() if '"ebn0_db"' in l]
+    assert len(d) == 1
+    col = d[0]["collectives"]
+    assert col["backend"] == "nccl" and col["world"] == 1, col
+    assert col["allreduce"] >= 2 and col["allgather"] >= 1, col     # rounds + the exact-stop cut round
+    q = subprocess.run([sys.executable, "-m", "ldpcsimulation_amd.sweep"] + args + ["--log", str(tmp_path / "plain.txt")],
+                       cwd=root, capture_output=True, text=True, timeout=600)
+    assert q.returncode == 0, q.stderr[-3000:]
+    e = [json.loads(l[l.index("{"):]) for l in q.stdout.splitlines() if '"ebn0_db"' in l]
+    assert e[0]["collectives"]["backend"] is None
+    keys = ("bit_err", "frame_err", "uncoded_bit_err", "frames", "iters", "syndrome_fail")
+    assert {k: d[0][k] for k in keys} == {k: e[0][k] for k in keys}
+    assert d[0]["frame_err"] >= 40 and d[0]["bit_err"] >= 200
+    assert (tmp_path / "nccl.txt").read_text() == (tmp_path / "plain.txt").read_text()
+
+
+@pytest.mark.gpu
+def test_bench_one_rank_rccl_line():
+    """bench.py --gpus 1 --backend nccl under a one-rank torchrun runs
+    its per-step RCCL all-reduce, barrier and max-over-ranks timing and prints a valid
+    line (the driver's 8-GPU launch is this command with --nproc-per-node 8)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = _torchrun1(root, ["bench.py", "--gpus", "1", "--backend", "nccl", "--steps", "2", "--warmup", "1",
+                          "--batch", "8192", "--no-cpu-baseline", "--no-secondary", "--live-pmc", "off"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["collective_backend"] == "nccl" and line["n_gpus"] == 1 and line["steps"] == 2
+    assert line["value"] > 0 and line["fer"]["frames"] == 2 * 8192
+    assert line["kernel_info"]["kernel"] == "rows_pp"
