@@ -12,7 +12,7 @@ HIPFLAGS  = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Iincl
 CXXFLAGS  = -O2 -std=c++17 -ffp-contract=off -Iinclude -Wall
 
 LIB       = $(LIBDIR)/libldpc_hip.so
-OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
+OBJS      = $(LIBDIR)/obj/kernels.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/nb_graph.o $(LIBDIR)/obj/api.o $(LIBDIR)/obj/graph.o
 CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalizedMinSum $(BINDIR)/decodeOffsetMinSum \
             $(BINDIR)/decodeMNGDBF $(BINDIR)/decodeSMNGDBF $(BINDIR)/decodeATGDBF $(BINDIR)/decodeSATGDBF $(BINDIR)/decodeSMGDBF $(BINDIR)/decodeBP \
             $(BINDIR)/decodeSGDBF $(BINDIR)/decodeMGDBF $(BINDIR)/decodeStochasticNGDBF
@@ -52,9 +52,11 @@ $(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/
 	$(HIPCC) $(HIPFLAGS) $(NOSLP) -c -o $@ $<
 $(LIBDIR)/obj/bp.o: $(CSRC)/bp.hip $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
-$(LIBDIR)/obj/nb.o: $(CSRC)/nb.hip $(CSRC)/nb.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
+$(LIBDIR)/obj/nb.o: $(CSRC)/nb.hip $(CSRC)/nb.h $(CSRC)/nb_layout.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(NOSLP) -c -o $@ $<
-$(LIBDIR)/obj/nb_api.o: $(CSRC)/nb_api.cpp $(CSRC)/nb.h $(CSRC)/kernels.h include/ldpc_hip.h | $(LIBDIR)/obj
+$(LIBDIR)/obj/nb_api.o: $(CSRC)/nb_api.cpp $(CSRC)/nb.h $(CSRC)/nb_layout.h $(CSRC)/nb_graph.h $(CSRC)/kernels.h include/ldpc_hip.h | $(LIBDIR)/obj
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+$(LIBDIR)/obj/nb_graph.o: $(CSRC)/nb_graph.cpp $(CSRC)/nb_graph.h $(CSRC)/nb_layout.h include/ldpc_hip.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/api.o: $(CSRC)/api.cpp $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/gdbf.h $(CSRC)/graph.h include/ldpc_hip.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -106,7 +108,7 @@ variant:
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(NOSLP) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
 	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/api.o $(CSRC)/api.cpp
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
-	    $(VARDIR)/obj_$(NAME)/kernels.o $(VARDIR)/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/graph.o
+	    $(VARDIR)/obj_$(NAME)/kernels.o $(VARDIR)/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/nb_graph.o $(LIBDIR)/obj/graph.o
 
 # Fast row kernel A/B variants: make fastvariant NAME=x VFLAGS="-DLDPC_FAST_..." -> ab/libldpc_hip_x.so
 fastvariant: $(OBJS)
@@ -162,13 +164,16 @@ clean:
 
 .PHONY: all oracle ref clean clean-ab variant fastvariant ppvariant nbvariant gdbfvariant bpvariant
 
-# Host-code sanitizer build: graph.cpp (the Tanner-graph compiler)
+# Host-code sanitizer build: graph.cpp (the Tanner-graph compiler), nb_graph.cpp
+# (the NB alist reader, GF tables, slot swizzles), cli_common.h (the CLIs' codeword files)
 # and the CPU oracle under AddressSanitizer + UBSan, driven over code files.
 ASAN_FLAGS = -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all
-build/host_asan: tests/native/host_asan.cpp $(CSRC)/graph.cpp $(CSRC)/graph.h oracle/ldpc_oracle.c oracle/ldpc_oracle.h
+build/host_asan: tests/native/host_asan.cpp $(CSRC)/graph.cpp $(CSRC)/graph.h $(CSRC)/nb_graph.cpp $(CSRC)/nb_graph.h \
+                 $(CSRC)/nb_layout.h $(CSRC)/cli_common.h oracle/ldpc_oracle.c oracle/ldpc_oracle.h
 	mkdir -p build
 	gcc $(ASAN_FLAGS) -std=c11 -ffp-contract=off -Ioracle -c -o build/ldpc_oracle_asan.o oracle/ldpc_oracle.c
-	g++ $(ASAN_FLAGS) -std=c++17 -I$(CSRC) -Ioracle -o $@ tests/native/host_asan.cpp $(CSRC)/graph.cpp build/ldpc_oracle_asan.o -lm
+	g++ $(ASAN_FLAGS) -std=c++17 -Iinclude -I$(CSRC) -Ioracle -o $@ tests/native/host_asan.cpp $(CSRC)/graph.cpp \
+	    $(CSRC)/nb_graph.cpp build/ldpc_oracle_asan.o -lm
 asan: build/host_asan
 	build/host_asan $(ASAN_CODES)
 .PHONY: asan

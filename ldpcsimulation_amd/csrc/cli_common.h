@@ -1,7 +1,9 @@
 // cli_common.h -- host helpers shared by the reference-compatible CLIs.
 #pragma once
+#include <cstdint>
 #include <fstream>
 #include <iterator>
+#include <ostream>
 #include <string>
 #include <vector>
 
@@ -30,4 +32,28 @@ inline std::vector<std::string> reference_codeword_lines(const char *path)
     }
     if (lines.empty()) lines.push_back(std::string());
     return lines;
+}
+
+// One codeword line into the bipolar transmitted word c[0..N) (decodeMinSum.cpp:202-211,
+// decodeGDBF.cpp:239-248): '1' -> -1, '0' -> +1; any other symbol, or a line shorter
+// than N, is reported on `log` and leaves c[i] as it was, as in the reference.
+inline void apply_codeword_line(const std::string &s, int N, std::vector<int8_t> &c, std::ostream &log)
+{
+    if ((int)c.size() < N) c.resize(N, 1);
+    for (int i = 0; i < N; ++i) {
+        const char ch = i < (int)s.size() ? s[i] : '\0';
+        if (ch == '1') c[i] = -1;
+        else if (ch == '0') c[i] = +1;
+        else log << "Got an invalid symbol at index " << i << std::endl;
+    }
+}
+
+// "N M / maxdv maxdc" as the alist header declares them (the dv, dc the reference
+// prints, decodeMinSum.cpp:150-151); a field that cannot be read is 0.
+inline void alist_header(const char *path, int &dv, int &dc)
+{
+    std::ifstream f(path);
+    int n = 0, m = 0;
+    dv = dc = 0;
+    f >> n >> m >> dv >> dc;
 }

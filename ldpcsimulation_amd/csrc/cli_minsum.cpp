@@ -73,13 +73,6 @@ void print_histogram(const std::vector<long> &h)   // printHistogram (:373-380)
 }
 
 // Read "N M / maxdv maxdc" as declared in the alist header (dv, dc of :150-151).
-void alist_header(const char *path, int &dv, int &dc)
-{
-    std::ifstream f(path);
-    int n = 0, m = 0;
-    dv = dc = 0;
-    f >> n >> m >> dv >> dc;
-}
 
 }  // namespace
 
@@ -213,13 +206,7 @@ int main(int argc, char *argv[])
     // is reported and leaves c[i] as it was, like the reference.
     std::vector<int8_t> c_cur(N, 1);
     auto load_codeword = [&](long frame, std::vector<int8_t> &c) {
-        const std::string &s = cw_lines[(size_t)(frame % (long)cw_lines.size())];
-        for (int i = 0; i < N; ++i) {
-            const char ch = i < (int)s.size() ? s[i] : '\0';
-            if (ch == '1') c[i] = -1;
-            else if (ch == '0') c[i] = +1;
-            else cout << "Got an invalid symbol at index " << i << endl;
-        }
+        apply_codeword_line(cw_lines[(size_t)(frame % (long)cw_lines.size())], N, c, cout);
     };
     if (philox && use_cw) {
         std::vector<uint8_t> bits((size_t)cw_lines.size() * N);

@@ -39,6 +39,13 @@ __device__ __forceinline__ void two_min(const double (&x)[DC], double &m1, doubl
     } else if constexpr (N == 2) {
         m1 = __builtin_fmin(__builtin_fabs(x[K0]), __builtin_fabs(x[K0 + 1]));
         m2 = __builtin_fmax(__builtin_fabs(x[K0]), __builtin_fabs(x[K0 + 1]));
+    } else if constexpr (N == 3) {
+        // 4 operations instead of the split's 6 (a one-element side would carry an
+        // m2 = +inf that the merge has to min away: fmin(inf, x) does not fold, NaN)
+        const double a = __builtin_fabs(x[K0]), b = __builtin_fabs(x[K0 + 1]), c = __builtin_fabs(x[K0 + 2]);
+        const double lo = __builtin_fmin(a, b), hi = __builtin_fmax(a, b);
+        m1 = __builtin_fmin(lo, c);
+        m2 = __builtin_fmin(hi, __builtin_fmax(lo, c));
     } else {
         constexpr int L = N / 2;
         double l1, l2, r1, r2;
@@ -76,6 +83,11 @@ __device__ __forceinline__ double norm64(double m, double alpha, double rcp, dou
 #ifndef LDPC_FAST64_STORE_VALU
 #define LDPC_FAST64_STORE_VALU 3
 #endif
+// ACC (the ping-pong kernel): instead of a per-row premise compare and flag, the row
+// folds hi32(M2) into a per-thread sticky maximum pacc (one v_max_u32; M2 >= +0 or NaN,
+// so M2 < 2^1000 <=> hi32(M2) < kFast64MaxHi as u32, NaN and inf above it), and a tiny
+// minimum forces pacc to ~0; the caller flags the codeword once, after its last
+// iteration (the flag is only read then). Same set of re-decoded codewords.
 struct NoSink {
     __device__ __forceinline__ void operator()(int, const Pack<double, 1> &) const {}
 };
@@ -83,9 +95,9 @@ struct NoSink {
 // with ORDER the scheduler is asked to keep that per-edge order (the selects of
 // edge k, then its store), so the stores start while later edges are computed
 // instead of trailing the whole row.
-template <int DC, int VAR, bool FDIV, int DCA, typename Sink = NoSink, bool ORDER = false>
+template <int DC, int VAR, bool FDIV, int DCA, typename Sink = NoSink, bool ORDER = false, bool ACC = false>
 __device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DCA], Pack<double, 1> (&pv)[DCA], double alpha,
-                                          double rcp, double delta, Sink sink = Sink())
+                                          double rcp, double delta, Sink sink = Sink(), uint32_t *pacc = nullptr)
 {
     static_assert(DC >= 1 && DC <= DCA, "cn_fast64 degree");
     constexpr uint32_t SIGN = 0x80000000u;
@@ -101,19 +113,33 @@ __device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DCA], Pac
     const double M1 = norm64<VAR, FDIV>(mn1, alpha, rcp, delta), M2 = norm64<VAR, FDIV>(mn2, alpha, rcp, delta);
     // M2 < 2^1000 (also false for NaN; M1 <= M2 covers the row). The u32 form compares the
     // high words (M2 >= +0; 2^1000's low word is 0).
+    bool ok = true;
+    if constexpr (ACC) {
+        const uint32_t h2 = hi32(M2);
+        *pacc = *pacc > h2 ? *pacc : h2;   // v_max_u32
+    } else {
 #if LDPC_FAST_INTPREM
-    bool ok = hi32(M2) < kFast64MaxHi;
+        ok = hi32(M2) < kFast64MaxHi;
 #else
-    bool ok = M2 < kFast64Max;
+        ok = M2 < kFast64Max;
 #endif
+    }
     if constexpr (VAR == V_NMS && FDIV) {
         // minima in (0, 2^-960): the one-FMA division may round wrongly (wave-uniform skip, rare)
 #if LDPC_FAST_INTPREM
-        if (__builtin_amdgcn_ballot_w64(hi32(mn1) < kFast64TinyHi))
+        if (__builtin_amdgcn_ballot_w64(hi32(mn1) < kFast64TinyHi)) {
 #else
-        if (__builtin_amdgcn_ballot_w64(mn1 < kFast64Tiny))
+        if (__builtin_amdgcn_ballot_w64(mn1 < kFast64Tiny)) {
 #endif
-            ok &= !(mn1 > 0.0 && mn1 < kFast64Tiny) & !(mn2 > 0.0 && mn2 < kFast64Tiny);
+            if constexpr (ACC) {
+                uint32_t t = *pacc;
+                asm volatile("" : "+v"(t));   // a side effect: the rare path stays a branch (not if-converted)
+                if ((mn1 > 0.0 && mn1 < kFast64Tiny) | (mn2 > 0.0 && mn2 < kFast64Tiny)) t = ~0u;
+                *pacc = t;
+            } else {
+                ok &= !(mn1 > 0.0 && mn1 < kFast64Tiny) & !(mn2 > 0.0 && mn2 < kFast64Tiny);
+            }
+        }
     }
     uint32_t mk1 = SIGN, mk2 = SIGN;
     if constexpr (VAR == V_OMS) {   // a zeroed message is +0, and sgn(-0.0) = +1 (:511-513)

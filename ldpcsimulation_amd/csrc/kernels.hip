@@ -23,10 +23,7 @@
 #include "device_common.h"
 // The fp32 row kernel (k_decode_rows) adds its pairs as one v_pk_add_f32: two plain
 // v_add_f32 measured 10.0 vs 8.8 ms per bench launch there (the ping-pong kernel is the
-// other way round: minsum_common.h).
-#ifndef LDPC_PK_ADD
-#define LDPC_PK_ADD 1
-#endif
+// other way round: minsum_common.h padd, template parameter PK).
 #include "minsum_common.h"
 
 #include <hip/hip_runtime.h>
@@ -1443,8 +1440,8 @@ __device__ __forceinline__ void cn_exact(const Pack<F, C> (&xin)[DC], int c, Pac
     }
 }
 
-template <int DC, int C>
-__device__ __forceinline__ bool cn_fast(const Pack<double, C> (&)[DC], Pack<double, C> (&)[DC], bool, float, float)
+template <int DC, int C, int DCA = DC, bool PK = false>
+__device__ __forceinline__ bool cn_fast(const Pack<double, C> (&)[DCA], Pack<double, C> (&)[DCA], bool, float, float)
 {
     return false;   // never called: fp64 always takes the exact path
 }
@@ -1660,7 +1657,7 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
                         for (int k = 0; k < DC; ++k) pv[k] = c2v[u16_at<DC>(posw[r], k)];
                     }
                     if constexpr (FAST) {
-                        const bool ok = cn_fast<DC, C>(xin[r & 1], pv, a.variant == V_NMS, (float)alpha, a.alpha_rcp);
+                        const bool ok = cn_fast<DC, C, DC, true>(xin[r & 1], pv, a.variant == V_NMS, (float)alpha, a.alpha_rcp);
                         // Rows past M (degree 0) only write the never-read dummy slots.
                         if (!ok && deg[r] > 0) red[31] = 1;
                     } else {
@@ -1687,7 +1684,7 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
 #pragma unroll
                     for (int i = 0; i < CPT; ++i) sum[i] = yq[i];
                     int k = 0;
-                    vn_phases<F, C, CPT, CPT>(c2v + lane, vgb, vgd, k, sum);
+                    vn_phases<F, C, CPT, CPT, true>(c2v + lane, vgb, vgd, k, sum);
 #pragma unroll
                     for (int i = 0; i < CPT; ++i) app[vdst(i)] = sum[i];
                 }

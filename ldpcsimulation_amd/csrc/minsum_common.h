@@ -10,10 +10,6 @@ namespace ldpc {
 
 enum { V_MS = 0, V_NMS = 1, V_OMS = 2 };
 
-// 1: fp32 pairs added as one packed v_pk_add_f32 (the round-1..3 code), 0: two v_add_f32.
-#ifndef LDPC_PK_ADD
-#define LDPC_PK_ADD 0
-#endif
 
 template <typename F> struct RowState;
 template <> struct __attribute__((aligned(16))) RowState<float> { float m1, m2; uint64_t meta; };
@@ -96,27 +92,31 @@ __device__ __forceinline__ float fsub32(float a, float b)
     return r;
 }
 
-// s += r for every codeword of a pack.
-template <typename F, int C>
+// s += r for every codeword of a pack. PK (fp32 pairs only): one packed v_pk_add_f32
+// -- the fp32 row kernel (kernels.hip k_decode_rows) keeps it, 8.8 vs 10.0 ms per bench
+// launch for two plain adds there -- else two v_add_f32 (the ping-pong and rows_fast
+// kernels: a packed add issues slower than the two plain ones on gfx950). The choice
+// is a template parameter, so one inline function never means two things in two
+// translation units. Same values either way.
+template <bool PK = false, typename F, int C>
 __device__ __forceinline__ void padd(Pack<F, C> &s, const Pack<F, C> &r)
 {
+    if constexpr (sizeof(F) == 4 && C == 2) {
+        if constexpr (PK) {
+            using V = float __attribute__((ext_vector_type(2)));
+            V a, b;
+            __builtin_memcpy(&a, &s, sizeof(V));
+            __builtin_memcpy(&b, &r, sizeof(V));
+            a += b;
+            __builtin_memcpy(&s, &a, sizeof(V));
+        } else {
+            s.v[0] = fadd32(s.v[0], r.v[0]);
+            s.v[1] = fadd32(s.v[1], r.v[1]);
+        }
+    } else {
 #pragma unroll
-    for (int c = 0; c < C; ++c) s.v[c] += r.v[c];
-}
-template <>
-__device__ __forceinline__ void padd<float, 2>(Pack<float, 2> &s, const Pack<float, 2> &r)
-{
-#if LDPC_PK_ADD
-    using V = float __attribute__((ext_vector_type(2)));
-    V a, b;
-    __builtin_memcpy(&a, &s, sizeof(V));
-    __builtin_memcpy(&b, &r, sizeof(V));
-    a += b;
-    __builtin_memcpy(&s, &a, sizeof(V));
-#else
-    s.v[0] = fadd32(s.v[0], r.v[0]);
-    s.v[1] = fadd32(s.v[1], r.v[1]);
-#endif
+        for (int c = 0; c < C; ++c) s.v[c] += r.v[c];
+    }
 }
 
 // Bit nodes, edges k in [k, kend) of the first NACT slots (every one of them has
@@ -141,15 +141,15 @@ __device__ __forceinline__ void vn_load(const Pack<F, C> *c2v, const int (&base)
 #pragma unroll
         for (int u = 0; u < U; ++u) r[i][u] = c2v[base[i] + (k + u) * 64];
 }
-template <typename F, int C, int NACT, int U, int CPT>
+template <typename F, int C, int NACT, int U, int CPT, bool PK = false>
 __device__ __forceinline__ void vn_add(const Pack<F, C> (&r)[NACT][U], Pack<F, C> (&sum)[CPT])
 {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int i = 0; i < NACT; ++i) padd(sum[i], r[i][u]);
+        for (int i = 0; i < NACT; ++i) padd<PK>(sum[i], r[i][u]);
 }
-template <typename F, int C, int NACT, int CPT>
+template <typename F, int C, int NACT, int CPT, bool PK = false>
 __device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base)[CPT], int &k, int kend,
                                          Pack<F, C> (&sum)[CPT])
 {
@@ -162,11 +162,11 @@ __device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base
             vn_load<F, C, NACT, U, CPT>(c2v, base, k, ra);
             for (;;) {
                 if (n >= 2) vn_load<F, C, NACT, U, CPT>(c2v, base, k + U, rb);
-                vn_add<F, C, NACT, U, CPT>(ra, sum);
+                vn_add<F, C, NACT, U, CPT, PK>(ra, sum);
                 k += U;
                 if (--n == 0) break;
                 if (n >= 2) vn_load<F, C, NACT, U, CPT>(c2v, base, k + U, ra);
-                vn_add<F, C, NACT, U, CPT>(rb, sum);
+                vn_add<F, C, NACT, U, CPT, PK>(rb, sum);
                 k += U;
                 if (--n == 0) break;
             }
@@ -181,22 +181,22 @@ __device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int i = 0; i < NACT; ++i) padd(sum[i], r[i][u]);
+            for (int i = 0; i < NACT; ++i) padd<PK>(sum[i], r[i][u]);
     }
     for (; k < kend; ++k) {
         Pack<F, C> r[NACT];
 #pragma unroll
         for (int i = 0; i < NACT; ++i) r[i] = c2v[base[i] + k * 64];
 #pragma unroll
-        for (int i = 0; i < NACT; ++i) padd(sum[i], r[i]);
+        for (int i = 0; i < NACT; ++i) padd<PK>(sum[i], r[i]);
     }
 }
-template <typename F, int C, int NACT, int CPT>
+template <typename F, int C, int NACT, int CPT, bool PK = false>
 __device__ __forceinline__ void vn_phases(const Pack<F, C> *c2v, const int (&base)[CPT], const int (&gd)[CPT], int &k,
                                           Pack<F, C> (&sum)[CPT])
 {
-    vn_phase<F, C, NACT, CPT>(c2v, base, k, gd[NACT - 1], sum);
-    if constexpr (NACT > 1) vn_phases<F, C, NACT - 1, CPT>(c2v, base, gd, k, sum);
+    vn_phase<F, C, NACT, CPT, PK>(c2v, base, k, gd[NACT - 1], sum);
+    if constexpr (NACT > 1) vn_phases<F, C, NACT - 1, CPT, PK>(c2v, base, gd, k, sum);
 }
 
 // Check node, fast fp32 path (MS, and NMS with a verified reciprocal). Exact
@@ -214,7 +214,8 @@ __device__ __forceinline__ void vn_phases(const Pack<F, C> *c2v, const int (&bas
 // 1e30 (or is inf), and the caller hands the block to the exact path before
 // the next iteration (keeping the premise true).
 // Edges [0, DC) of arrays of extent DCA >= DC (the entries past DC are not touched).
-template <int DC, int C, int DCA = DC>
+// PK: the v2c of a pair as one v_pk_add_f32 (see padd).
+template <int DC, int C, int DCA = DC, bool PK = false>
 __device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DCA], Pack<float, C> (&pv)[DCA], bool nms,
                                         float alpha, float rcp)
 {
@@ -224,15 +225,15 @@ __device__ __forceinline__ bool cn_fast(const Pack<float, C> (&xin)[DCA], Pack<f
     V x[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-#if LDPC_PK_ADD
-        V xi, pi;
-        __builtin_memcpy(&xi, &xin[k], sizeof(V));
-        __builtin_memcpy(&pi, &pv[k], sizeof(V));
-        x[k] = xi - pi;                                                         // v2c (:469)
-#else
+        if constexpr (PK) {
+            V xi, pi;
+            __builtin_memcpy(&xi, &xin[k], sizeof(V));
+            __builtin_memcpy(&pi, &pv[k], sizeof(V));
+            x[k] = xi - pi;                                                         // v2c (:469)
+        } else {
 #pragma unroll
-        for (int c = 0; c < C; ++c) x[k][c] = fsub32(xin[k].v[c], pv[k].v[c]);   // v2c (:469), one v_sub_f32 each
-#endif
+            for (int c = 0; c < C; ++c) x[k][c] = fsub32(xin[k].v[c], pv[k].v[c]);   // v2c (:469), one v_sub_f32 each
+        }
     }
     bool ok = true;
 #pragma unroll

@@ -5,10 +5,9 @@
 #include <cstdint>
 #include <string>
 
-namespace ldpc {
+#include "nb_layout.h"
 
-constexpr int kNbQ = 16;          // field size the kernels are built for (GF(16), BASELINE config 5)
-constexpr int kNbMaxDc = 8;       // row degree bound (DC template 4 / 8)
+namespace ldpc {
 
 struct NbDevGraph {
     int N, M, q, m, E, maxdc;
@@ -42,25 +41,8 @@ struct NbChoice {
     size_t slot_bytes = 0;        // ems_global: message bytes per resident codeword
 };
 
-// Position-major message slot count (maxdc * M) rounded up to a power of two
-// (at least 4): the chunk stride of the message layout of nb.hip, where the byte
-// offset of entry p of slot s is (s << 4) ^ nb_lambda(p) -- XOR-linear in p.
-__host__ __device__ inline int nb_ep(const NbDevGraph &g)
-{
-    int e = 4;
-    while (e < g.maxdc * g.M) e <<= 1;
-    return e;
-}
-__host__ __device__ inline int nb_ep_log2(int ep)
-{
-    int k = 0;
-    while ((1 << k) < ep) ++k;
-    return k;
-}
-// Byte offset of entry p (0..15) relative to its slot's s << 4, chunk stride 2^k slots:
-// chunk p >> 2 at (p >> 2) << (k + 4), the slot XOR-ed with the chunk index (bits 4-5),
-// the entry within its 16-byte chunk at (p & 3) << 2.
-__host__ __device__ inline int nb_lambda(int p, int k) { return (p << 2) ^ ((p >> 2) << (k + 4)); }
+// the chunk stride of a device graph's message layout (nb_layout.h)
+__host__ __device__ inline int nb_ep(const NbDevGraph &g) { return nb_ep(g.maxdc, g.M); }
 
 NbChoice nb_choose(const NbDevGraph &g, int maxdc);
 hipError_t nb_launch(const NbDevGraph &g, const NbArgs &a, const NbChoice &ch, void *scratch, int slots,

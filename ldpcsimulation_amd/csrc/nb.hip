@@ -655,7 +655,10 @@ NbChoice nb_choose(const NbDevGraph &g, int maxdc)
         if (opt(LDPC_OPT_EMS_THREADS) == 512) ch.threads = 512;
     }
     const size_t aux = aux_bytes(g), msgb = align16((size_t)nb_ep(g) * g.q * 4);
-    if (maxdc > kNbMaxDc || aux > kNbMaxLds || nb_ep(g) > 65535 || g.N > 65535) {
+    // The 16-bit schedule entries are the slot indices (< maxdc * M: vslot) and the
+    // symbols (< N); the chunk stride Ep (maxdc * M rounded up to a power of two, up to
+    // 65 536) only enters int offsets.
+    if (maxdc > kNbMaxDc || aux > kNbMaxLds || (long)g.maxdc * g.M > 65535 || g.N > 65535) {
         ch.name = "";   // unsupported: degree, LDS schedule or 16-bit indices
         return ch;
     }
@@ -677,6 +680,15 @@ static hipError_t launch_t(const NbDevGraph &g, const NbArgs &a, const NbChoice 
     auto fn = (DC == 4 && ch.threads == 1024) ? k_ems<kNbQ, 4, DC, SRC, GS, 1024> : k_ems<kNbQ, 4, DC, SRC, GS, 512>;
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, ch.lds_bytes);
     if (e != hipSuccess) return e;
+    if (!GS) {
+        // MsgAddr XOR-s the message base into its offsets, which equals adding it only while
+        // the messages sit at LDS address 0: a static __shared__ in k_ems (or in a helper it
+        // inlines) would move the dynamic area and corrupt messages silently. Refuse instead.
+        hipFuncAttributes fa;
+        e = hipFuncGetAttributes(&fa, (const void *)fn);
+        if (e != hipSuccess) return e;
+        if (fa.sharedSizeBytes != 0) return hipErrorInvalidDeviceFunction;
+    }
     hipLaunchKernelGGL(fn, dim3(grid), dim3(ch.threads), ch.lds_bytes, s, a, g, (float *)scratch,
                        ch.slot_bytes / 4);
     return hipGetLastError();

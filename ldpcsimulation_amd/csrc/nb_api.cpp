@@ -4,6 +4,7 @@
 // contexts, decode of given channel samples and the fused Monte-Carlo.
 #include "ldpc_hip.h"
 #include "nb.h"
+#include "nb_graph.h"
 #include "kernels.h"
 
 #include <hip/hip_runtime.h>
@@ -14,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -62,32 +64,6 @@ struct Buf {
     }
 };
 
-int gf_poly(int q)
-{
-    switch (q) {
-    case 2: return 0x3;
-    case 4: return 0x7;
-    case 8: return 0xB;
-    case 16: return 0x13;
-    case 32: return 0x25;
-    case 64: return 0x43;
-    default: return 0;
-    }
-}
-
-int gf_mul(int q, int a, int b)
-{
-    const int poly = gf_poly(q);
-    int r = 0;
-    while (b) {
-        if (b & 1) r ^= a;
-        b >>= 1;
-        a <<= 1;
-        if (a & q) a ^= poly;
-    }
-    return r;
-}
-
 bool is_device_ptr(const void *p)
 {
     if (!p) return false;
@@ -100,12 +76,6 @@ bool is_device_ptr(const void *p)
 }
 
 }  // namespace
-
-struct ldpc_nb_graph {
-    int N = 0, M = 0, q = 0, m = 0, E = 0, maxdv = 0, maxdc = 0;
-    std::vector<int32_t> row_ptr, row_col, col_ptr, col_slot;
-    std::vector<uint8_t> row_h;
-};
 
 struct ldpc_nb_ctx {
     int device = 0, max_batch = 0, num_cus = 0;
@@ -122,139 +92,6 @@ struct ldpc_nb_ctx {
 // LDPC_OPT_EMS_SWIZZLE = 1 keeps the plain message layout (A/B).
 static bool nb_swizzle_enabled() { return ldpc::opt(LDPC_OPT_EMS_SWIZZLE) != 1; }
 
-// XOR swizzles of the message slots for the symbol-node gathers of nb.hip
-// (vn_lane: entry a of an edge is read at check-domain position (h*a) ^ f,
-// one ds_read_b32 per entry, the lanes of a wave on consecutive symbols).
-// Those gathers hit random banks in the plain layout (f = 0): 3.7 LDS cycles
-// per 32-lane group against 1 conflict-free (GF(16) N=1000 code). A local
-// search picks f per slot under the constraint that the XOR of f over every
-// check's slots is 0 (what keeps the check node's outputs in place), scoring
-// the LDS bank model of the gathers: two groups of 32 lanes, bank = dword mod
-// 32, cost = the most-used bank. Moves XOR the same delta into two slots of one
-// check. Deterministic (fixed seed). Returned: col_h | f << 4 per column entry.
-static std::vector<uint8_t> nb_swizzled_coefficients(const ldpc_nb_graph &g, const std::vector<int32_t> &pslot,
-                                                     const std::vector<uint8_t> &colh, const std::vector<uint8_t> &mul)
-{
-    std::vector<uint8_t> out(colh);
-    if (g.q != ldpc::kNbQ || g.E == 0) return out;
-    const int Q = g.q, N = g.N, M = g.M, DV = std::max(g.maxdv, 1);
-    ldpc::NbDevGraph shape{};
-    shape.maxdc = g.maxdc;
-    shape.M = M;
-    const int lg = ldpc::nb_ep_log2(ldpc::nb_ep(shape));
-    std::vector<uint8_t> f((size_t)g.maxdc * M, 0);
-    std::vector<int> slot_v(f.size(), -1), slot_k(f.size(), 0);
-    for (int v = 0; v < N; ++v)
-        for (int e = g.col_ptr[v]; e < g.col_ptr[v + 1]; ++e) {
-            slot_v[pslot[e]] = v;
-            slot_k[pslot[e]] = e - g.col_ptr[v];
-        }
-    auto gcost = [&](int grp, int k) {   // summed over the Q entries of edge index k of a 32-symbol group
-        int tot = 0;
-        for (int a = 0; a < Q; ++a) {
-            int cnt[32] = {0}, mx = 0;
-            for (int v = grp * 32; v < std::min(N, grp * 32 + 32); ++v) {
-                const int e = g.col_ptr[v] + k;
-                if (e >= g.col_ptr[v + 1]) continue;
-                const int sl = pslot[e], p = mul[(size_t)colh[e] * Q + a] ^ f[sl];
-                mx = std::max(mx, ++cnt[((((unsigned)sl << 4) ^ (unsigned)ldpc::nb_lambda(p, lg)) >> 2) & 31]);
-            }
-            tot += mx;
-        }
-        return tot;
-    };
-    const int ngroups = (N + 31) / 32;
-    std::vector<int> C((size_t)ngroups * DV);
-    for (int grp = 0; grp < ngroups; ++grp)
-        for (int k = 0; k < DV; ++k) C[(size_t)grp * DV + k] = gcost(grp, k);
-    uint32_t x = 0x9e3779b9u;
-    auto rnd = [&]() { x ^= x << 13; x ^= x >> 17; x ^= x << 5; return x; };
-    // a move needs two slots of one check: only checks of degree >= 2 take part
-    std::vector<int> rows2;
-    for (int j = 0; j < M; ++j)
-        if (g.row_ptr[j + 1] - g.row_ptr[j] >= 2) rows2.push_back(j);
-    if (rows2.empty()) return out;
-    const long moves = std::min(200000L, 40L * g.E);
-    for (long it = 0; it < moves; ++it) {
-        const int j = rows2[rnd() % (uint32_t)rows2.size()], d = g.row_ptr[j + 1] - g.row_ptr[j];
-        const int k1 = (int)(rnd() % (uint32_t)d);
-        int k2 = (int)(rnd() % (uint32_t)(d - 1));
-        if (k2 >= k1) ++k2;
-        const uint8_t delta = (uint8_t)(1 + rnd() % (uint32_t)(Q - 1));
-        const int s1 = k1 * M + j, s2 = k2 * M + j;
-        const int a1 = (slot_v[s1] / 32) * DV + slot_k[s1], a2 = (slot_v[s2] / 32) * DV + slot_k[s2];
-        const int before = C[a1] + (a2 != a1 ? C[a2] : 0);
-        f[s1] ^= delta;
-        f[s2] ^= delta;
-        const int n1 = gcost(a1 / DV, a1 % DV), n2 = a2 != a1 ? gcost(a2 / DV, a2 % DV) : 0;
-        if (n1 + n2 <= before) {
-            C[a1] = n1;
-            if (a2 != a1) C[a2] = n2;
-        } else {
-            f[s1] ^= delta;
-            f[s2] ^= delta;
-        }
-    }
-    for (int e = 0; e < g.E; ++e) out[e] = (uint8_t)(colh[e] | (f[pslot[e]] << 4));
-    return out;
-}
-
-// Build the CSR views from (row, value) lists per column and (column, value) per row (0-based).
-static int build_nb(int N, int M, int q, const std::vector<std::vector<std::pair<int, int>>> &cols,
-                    const std::vector<std::vector<std::pair<int, int>>> &rows, ldpc_nb_graph &g)
-{
-    if (N <= 0 || M <= 0) return err(LDPC_ERR_GRAPH, "bad dimensions N=%d M=%d", N, M);
-    if (!gf_poly(q)) return err(LDPC_ERR_GRAPH, "q=%d is not a supported power of two (2..64)", q);
-    g.N = N;
-    g.M = M;
-    g.q = q;
-    g.m = 0;
-    while ((1 << g.m) < q) ++g.m;
-    g.row_ptr.assign(M + 1, 0);
-    for (int j = 0; j < M; ++j) {
-        if (rows[j].size() < 2) return err(LDPC_ERR_GRAPH, "check %d has degree %zu (< 2)", j, rows[j].size());
-        g.row_ptr[j + 1] = g.row_ptr[j] + (int)rows[j].size();
-        g.maxdc = std::max(g.maxdc, (int)rows[j].size());
-    }
-    g.E = g.row_ptr[M];
-    g.row_col.resize(g.E);
-    g.row_h.resize(g.E);
-    std::vector<std::vector<std::pair<int, int>>> seen(N);   // (row, h) pairs from the row view
-    for (int j = 0; j < M; ++j)
-        for (size_t k = 0; k < rows[j].size(); ++k) {
-            const int c = rows[j][k].first, h = rows[j][k].second;
-            if (c < 0 || c >= N) return err(LDPC_ERR_GRAPH, "check %d: symbol index %d out of range", j, c + 1);
-            if (h <= 0 || h >= q) return err(LDPC_ERR_GRAPH, "check %d: coefficient %d outside 1..q-1", j, h);
-            for (const auto &pr : seen[c])
-                if (pr.first == j) return err(LDPC_ERR_GRAPH, "check %d lists symbol %d twice", j, c + 1);
-            g.row_col[g.row_ptr[j] + k] = c;
-            g.row_h[g.row_ptr[j] + k] = (uint8_t)h;
-            seen[c].push_back({j, (int)(g.row_ptr[j] + k)});
-        }
-    g.col_ptr.assign(N + 1, 0);
-    g.col_slot.clear();
-    g.col_slot.reserve(g.E);
-    for (int i = 0; i < N; ++i) {
-        if (cols[i].size() != seen[i].size())
-            return err(LDPC_ERR_GRAPH, "symbol %d: column weight %zu but %zu rows list it", i + 1, cols[i].size(),
-                       seen[i].size());
-        for (const auto &ce : cols[i]) {
-            const int j = ce.first;
-            int slot = -1;
-            for (const auto &pr : seen[i])
-                if (pr.first == j) slot = pr.second;
-            if (slot < 0) return err(LDPC_ERR_GRAPH, "symbol %d lists check %d, which does not list it", i + 1, j + 1);
-            if (g.row_h[slot] != ce.second)
-                return err(LDPC_ERR_GRAPH, "edge (%d,%d): coefficient %d in the column view, %d in the row view",
-                           j + 1, i + 1, ce.second, g.row_h[slot]);
-            g.col_slot.push_back(slot);
-        }
-        g.col_ptr[i + 1] = (int)g.col_slot.size();
-        g.maxdv = std::max(g.maxdv, (int)cols[i].size());
-    }
-    return LDPC_OK;
-}
-
 extern "C" {
 
 int ldpc_nb_graph_create(int N, int M, int q, const int *num_nlist, const int *const *nlist, const int *const *nvals,
@@ -265,18 +102,16 @@ int ldpc_nb_graph_create(int N, int M, int q, const int *num_nlist, const int *c
     *out = nullptr;
     if (N <= 0 || M <= 0) return err(LDPC_ERR_GRAPH, "bad dimensions N=%d M=%d", N, M);
     try {
-        std::vector<std::vector<std::pair<int, int>>> cols(N), rows(M);
+        ldpc::NbLists cols(N), rows(M);
         for (int i = 0; i < N; ++i)
             for (int k = 0; k < num_nlist[i]; ++k) cols[i].push_back({nlist[i][k] - 1, nvals[i][k]});
         for (int j = 0; j < M; ++j)
             for (int k = 0; k < num_mlist[j]; ++k) rows[j].push_back({mlist[j][k] - 1, mvals[j][k]});
-        auto *g = new ldpc_nb_graph();
-        const int rc = build_nb(N, M, q, cols, rows, *g);
-        if (rc) {
-            delete g;
-            return rc;
-        }
-        *out = g;
+        std::unique_ptr<ldpc_nb_graph> g(new ldpc_nb_graph());
+        std::string msg;
+        const int rc = ldpc::nb_build_graph(N, M, q, cols, rows, *g, msg);
+        if (rc) return err(rc, "%s", msg.c_str());
+        *out = g.release();
     } catch (const std::bad_alloc &) {
         return err(LDPC_ERR_NOMEM, "graph build out of memory");
     }
@@ -287,42 +122,12 @@ int ldpc_nb_graph_load_alist(const char *path, ldpc_nb_graph **out)
 {
     if (!path || !out) return err(LDPC_ERR_INVALID, "null argument");
     *out = nullptr;
-    FILE *f = std::fopen(path, "r");
-    if (!f) return err(LDPC_ERR_IO, "cannot open %s", path);
-    auto rd = [&](int &v) { return std::fscanf(f, "%d", &v) == 1; };
-    int N = 0, M = 0, q = 0, dv = 0, dc = 0;
-    if (!rd(N) || !rd(M) || !rd(q) || !rd(dv) || !rd(dc) || N <= 0 || M <= 0 || dv <= 0 || dc <= 0 ||
-        N > (1 << 26) || M > (1 << 26) || dv > 1024 || dc > 1024) {
-        std::fclose(f);
-        return err(LDPC_ERR_GRAPH, "%s: bad NB alist header", path);
-    }
     try {
-        std::vector<int> wn(N), wm(M);
-        bool ok = true;
-        for (int i = 0; i < N && ok; ++i) ok = rd(wn[i]) && wn[i] >= 0 && wn[i] <= dv;
-        for (int j = 0; j < M && ok; ++j) ok = rd(wm[j]) && wm[j] >= 0 && wm[j] <= dc;
-        std::vector<std::vector<std::pair<int, int>>> cols(N), rows(M);
-        for (int i = 0; i < N && ok; ++i)
-            for (int k = 0; k < dv && ok; ++k) {
-                int a = 0, b = 0;
-                ok = rd(a) && rd(b);
-                if (k < wn[i]) cols[i].push_back({a - 1, b});
-            }
-        for (int j = 0; j < M && ok; ++j)
-            for (int k = 0; k < dc && ok; ++k) {
-                int a = 0, b = 0;
-                ok = rd(a) && rd(b);
-                if (k < wm[j]) rows[j].push_back({a - 1, b});
-            }
-        std::fclose(f);
-        if (!ok) return err(LDPC_ERR_GRAPH, "%s: truncated or malformed NB alist", path);
-        auto *g = new ldpc_nb_graph();
-        const int rc = build_nb(N, M, q, cols, rows, *g);
-        if (rc) {
-            delete g;
-            return rc;
-        }
-        *out = g;
+        std::unique_ptr<ldpc_nb_graph> g(new ldpc_nb_graph());
+        std::string msg;
+        const int rc = ldpc::nb_read_alist(path, *g, msg);
+        if (rc) return err(rc, "%s", msg.c_str());
+        *out = g.release();
     } catch (const std::bad_alloc &) {
         return err(LDPC_ERR_NOMEM, "alist load out of memory");
     }
@@ -367,26 +172,13 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
     c->stream = c->own;
     NB_HIP_TRY(hipEventCreate(&c->ev0));
     NB_HIP_TRY(hipEventCreate(&c->ev1));
-    // graph upload: row_ptr | row_col | col_ptr | col_slot | row_h | gf_mul | gf_inv
+    // graph upload: row_ptr | row_col | col_ptr | col_slot | row_h | gf_mul | gf_inv | pslot | colh | colh_swz
     const int q = g->q;
-    std::vector<uint8_t> mul((size_t)q * q), inv(q, 0);
-    for (int a = 0; a < q; ++a)
-        for (int b = 0; b < q; ++b) {
-            mul[(size_t)a * q + b] = (uint8_t)gf_mul(q, a, b);
-            if (mul[(size_t)a * q + b] == 1) inv[a] = (uint8_t)b;
-        }
+    ldpc::NbTables tb;
+    ldpc::nb_tables(*g, tb);
+    const std::vector<uint8_t> &mul = tb.mul, &inv = tb.inv, &colh = tb.colh, &colhs = tb.colh_swz;
+    const std::vector<int32_t> &pslot = tb.pslot;
     const size_t n_rp = (g->M + 1) * 4, n_rc = (size_t)g->E * 4, n_cp = (g->N + 1) * 4, n_cs = (size_t)g->E * 4;
-    // position-major slot (k*M + j) and coefficient of every column entry
-    std::vector<int32_t> pslot(g->E);
-    std::vector<uint8_t> colh(g->E);
-    for (int j = 0; j < g->M; ++j)
-        for (int r = g->row_ptr[j]; r < g->row_ptr[j + 1]; ++r)
-            for (int e = g->col_ptr[g->row_col[r]]; e < g->col_ptr[g->row_col[r] + 1]; ++e)
-                if (g->col_slot[e] == r) {
-                    pslot[e] = (r - g->row_ptr[j]) * g->M + j;
-                    colh[e] = g->row_h[r];
-                }
-    const std::vector<uint8_t> colhs = nb_swizzled_coefficients(*g, pslot, colh, mul);
     const size_t total = n_rp + n_rc + n_cp + 2 * n_cs + 3 * (size_t)g->E + mul.size() + inv.size() + 256;
     std::vector<uint8_t> blob(total, 0);
     size_t off = 0;

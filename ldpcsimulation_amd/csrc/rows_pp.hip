@@ -266,12 +266,16 @@ __device__ __forceinline__ void pp_account(const DecodeArgs &a, int *red, int gr
 // store(k, message) scatters the new message of edge k, called as each message is
 // formed, in per-edge order (LDPC_PP_STORE_ORDER), so the scatters overlap the selects
 // of the later edges (fp64: cn_fast64; fp32 pairs: cn_fast_pair).
+// fp64: the premise is folded into the slot's sticky hi-word maximum pacc (fast64.h ACC)
+// and checked once per codeword, after its last iteration (the slot flag is read only
+// then); the returned value is always true.
 template <typename F, int DC, int VAR, bool FDIV, int C, int DCA, typename Store>
 __device__ __forceinline__ bool pp_check_node(const Pack<F, C> (&xin)[DCA], Pack<F, C> (&pv)[DCA], F alpha, F rcp,
-                                              F delta, Store store)
+                                              F delta, Store store, uint32_t *pacc)
 {
     if constexpr (sizeof(F) == 8) {
-        return cn_fast64<DC, VAR, FDIV, DCA, Store, LDPC_PP_STORE_ORDER != 0>(xin, pv, alpha, rcp, delta, store);
+        return cn_fast64<DC, VAR, FDIV, DCA, Store, LDPC_PP_STORE_ORDER != 0, true>(xin, pv, alpha, rcp, delta, store,
+                                                                                     pacc);
     } else {
         return cn_fast_pair<DC, DCA, Store, LDPC_PP_STORE_ORDER != 0>(xin, pv, VAR == V_NMS, alpha, rcp, store);
     }
@@ -348,6 +352,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
     const int nsteps = (a.batch + 2 * C - 1) / (2 * C);
     PP_STAMP_DECL;
     for (int grp = blockIdx.x; grp < nsteps; grp += gridDim.x) {
+        [[maybe_unused]] uint32_t pacc[2] = {0u, 0u};   // fp64: per-slot sticky premise maximum (pp_check_node)
         int unc[2 * C];
 #pragma unroll
         for (int q = 0; q < 2 * C; ++q) unc[q] = 0;
@@ -461,7 +466,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                                 store(k, prev[X][r][k]);
                             }
                         } else {
-                            ok = pp_check_node<F, DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta, store);
+                            ok = pp_check_node<F, DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta, store, &pacc[X]);
                         }
                         if (!ok && deg[r] > 0 && LDPC_PP_EXP == 0) s.red[X] = 1;   // experiments: never re-decode
                         if (R > 1 && LDPC_PP_ROWFENCE) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
@@ -478,6 +483,10 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
         if (a.T > 0) {
             interval(std::integral_constant<int, 0>(), false, true);
             PP_BARRIER();   // | -- | bit(1,T-1) |
+        }
+        if constexpr (F64 && R > 0) {   // the premise of every iteration of the step (fast64.h ACC)
+            if (pacc[0] >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[0] = 1;
+            if (pacc[1] >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[1] = 1;
         }
 
         // syndrome (rows; padding edges read +inf: parity 0; rows past M skipped) and

@@ -9,4 +9,4 @@ $H -Xclang -target-feature -Xclang -load-store-opt -falign-loops=32 -mllvm -amdg
     -c -o $V/obj_ppst/rows_pp.o ldpcsimulation_amd/csrc/rows_pp.hip 2>/dev/null
 $H -c -o $V/obj_ppst/api.o ldpcsimulation_amd/csrc/api.cpp 2>/dev/null
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $V/libldpc_hip_ppst.so $L/obj/kernels.o $L/obj/rows_fast.o \
-    $V/obj_ppst/rows_pp.o $L/obj/gdbf.o $L/obj/bp.o $L/obj/nb.o $L/obj/nb_api.o $V/obj_ppst/api.o $L/obj/graph.o
+    $V/obj_ppst/rows_pp.o $L/obj/gdbf.o $L/obj/bp.o $L/obj/nb.o $L/obj/nb_api.o $L/obj/nb_graph.o $V/obj_ppst/api.o $L/obj/graph.o

@@ -1,14 +1,23 @@
 // Host-code sanitizer pass: the Tanner-graph compiler of
 // libldpc_hip.so (ldpcsimulation_amd/csrc/graph.cpp: load_alist, build_graph,
-// build_row_schedule, build_flood_schedule, build_layers) and the CPU oracle
-// (oracle/*.c) built with -fsanitize=address,undefined and run over every code
-// given on the command line, plus malformed inputs. Built and run by
-// `make asan` (tests/test_host_asan.py); any sanitizer report aborts with a
-// non-zero status.
+// build_row_schedule, build_flood_schedule, build_layers), the GF(q) graph code
+// of the EMS decoder (nb_graph.cpp: the NB alist reader, the CSR build, the GF
+// tables and the message-slot swizzle search), the CLIs' argument-file parsing
+// (cli_common.h: codeword files, alist headers) and the CPU oracle (oracle/*.c),
+// built with -fsanitize=address,undefined and run over every code given on the
+// command line, plus malformed inputs. Built and run by `make asan`
+// (tests/test_host_asan.py); any sanitizer report aborts with a non-zero status.
+//   usage: host_asan [binary.alist ...] [--nb nb.alist ...] [--cw codeword-file ...] [--tmp DIR]
 #include "graph.h"
+#include "nb_graph.h"
+#include "nb_layout.h"
+#include "cli_common.h"
+#include "ldpc_hip.h"
 extern "C" {
 #include "ldpc_oracle.h"
 }
+
+#include <sstream>
 
 #include <cmath>
 #include <cstdio>
@@ -110,9 +119,153 @@ static void one_code(const char *path)
     orc_alist_free(&H);
 }
 
+// An NB alist (SystemC/NB-LDPC/src/alist.cpp:23-56 format) through the loader and,
+// when it loads, the tables the EMS context uploads; GF(16) codes get the slot swizzle,
+// whose per-check XOR must be 0 (what keeps the check node's outputs in place).
+static void one_nb(const char *path)
+{
+    ldpc_nb_graph g;
+    std::string msg;
+    const int rc = ldpc::nb_read_alist(path, g, msg);
+    if (rc != LDPC_OK) {
+        std::printf("%s: NB rejected (%d: %s)\n", path, rc, msg.c_str());
+        CHECK(!msg.empty(), "%s: rejection without a message", path);
+        return;
+    }
+    CHECK(g.row_ptr.size() == (size_t)g.M + 1 && g.col_ptr.size() == (size_t)g.N + 1 && (int)g.col_slot.size() == g.E,
+          "%s: NB CSR sizes", path);
+    ldpc::NbTables t;
+    ldpc::nb_tables(g, t);
+    CHECK((int)t.pslot.size() == g.E && (int)t.colh_swz.size() == g.E, "%s: NB tables", path);
+    for (int a = 1; a < g.q; ++a) CHECK(t.mul[(size_t)a * g.q + t.inv[a]] == 1, "%s: GF inverse of %d", path, a);
+    if (g.q == ldpc::kNbQ) {
+        std::vector<int> x(g.M, 0);
+        for (int e = 0; e < g.E; ++e) {
+            CHECK((t.colh_swz[e] & 15) == t.colh[e], "%s: swizzle changed a coefficient", path);
+            x[t.pslot[e] % g.M] ^= t.colh_swz[e] >> 4;
+        }
+        for (int j = 0; j < g.M; ++j) CHECK(x[j] == 0, "%s: check %d swizzles do not XOR to 0", path, j);
+    }
+    std::printf("%s: NB N=%d M=%d q=%d E=%d maxdv=%d maxdc=%d\n", path, g.N, g.M, g.q, g.E, g.maxdv, g.maxdc);
+}
+
+static std::string write_tmp(const std::string &dir, const std::string &name, const std::string &text)
+{
+    const std::string p = dir + "/" + name;
+    FILE *f = std::fopen(p.c_str(), "wb");
+    if (!f) { std::printf("FAIL: cannot write %s\n", p.c_str()); ++fails; return p; }
+    std::fwrite(text.data(), 1, text.size(), f);
+    std::fclose(f);
+    return p;
+}
+
+// Malformed NB alists: each must be rejected with a message (never a crash).
+static void nb_malformed(const std::string &dir)
+{
+    const char *bad[][2] = {
+        {"empty", ""},
+        {"header_only", "4 2 16\n2 4\n"},
+        {"truncated", "4 2 16\n1 2\n1 1 1 1\n2 2\n1 3 0 0\n"},
+        {"neg_header", "-4 2 16\n1 2\n"},
+        {"huge_header", "100000000 2 16\n1 2\n"},
+        {"q_not_pow2", "2 1 12\n1 2\n1 1\n2\n1 3 0 0\n1 3\n1 3 2 3\n"},
+        {"degree1_check", "2 2 16\n1 1\n1 1\n1 1\n1 3\n2 4\n1 3\n2 4\n"},
+        {"degree0_check", "2 2 16\n1 2\n1 1\n2 0\n1 3\n1 4\n1 3 2 4\n0 0 0 0\n"},
+        {"index_out_of_range", "2 1 16\n1 2\n1 1\n2\n1 3\n1 4\n1 3 7 4\n"},
+        {"coef_zero", "2 1 16\n1 2\n1 1\n2\n1 0\n1 4\n1 0 2 4\n"},
+        {"coef_q", "2 1 16\n1 2\n1 1\n2\n1 16\n1 4\n1 16 2 4\n"},
+        {"views_disagree", "2 1 16\n1 2\n1 1\n2\n1 3\n1 4\n1 5 2 4\n"},
+        {"weight_above_max", "2 1 16\n1 2\n3 1\n2\n1 3\n1 4\n1 3 2 4\n"},
+        {"weight_negative", "2 1 16\n1 2\n-1 1\n2\n1 3\n1 4\n1 3 2 4\n"},
+        {"text", "this is not an alist\n"},
+    };
+    for (const auto &b : bad) {
+        const std::string p = write_tmp(dir, std::string("nb_") + b[0] + ".alist", b[1]);
+        ldpc_nb_graph g;
+        std::string msg;
+        const int rc = ldpc::nb_read_alist(p.c_str(), g, msg);
+        CHECK(rc == LDPC_ERR_GRAPH && !msg.empty(), "NB %s accepted (rc %d)", b[0], rc);
+    }
+    // a valid two-symbol GF(16) code, then the same through the list interface
+    const std::string ok = write_tmp(dir, "nb_ok.alist", "2 1 16\n1 2\n1 1\n2\n1 3\n1 4\n1 3 2 4\n");
+    ldpc_nb_graph g;
+    std::string msg;
+    CHECK(ldpc::nb_read_alist(ok.c_str(), g, msg) == LDPC_OK, "NB valid code rejected (%s)", msg.c_str());
+    ldpc::NbTables t;
+    if (g.E) ldpc::nb_tables(g, t);
+    ldpc_nb_graph g2;
+    CHECK(ldpc::nb_build_graph(2, 1, 16, {{{0, 3}}, {{0, 4}}}, {{{0, 3}, {1, 4}}}, g2, msg) == LDPC_OK, "NB lists");
+    CHECK(ldpc::nb_build_graph(0, 1, 16, {}, {{}}, g2, msg) == LDPC_ERR_GRAPH, "NB N = 0 accepted");
+    CHECK(ldpc::nb_read_alist((dir + "/does_not_exist.alist").c_str(), g2, msg) == LDPC_ERR_IO, "NB missing file");
+    for (int q : {2, 4, 8, 16, 32, 64})   // every field: a * inv(a) = 1 through the tables
+        for (int a = 1; a < q; ++a) {
+            int inv = 0;
+            for (int b = 1; b < q; ++b) if (ldpc::gf_mul(q, a, b) == 1) inv = b;
+            CHECK(inv != 0, "GF(%d): %d has no inverse", q, a);
+        }
+    CHECK(ldpc::nb_ep(4, 8200) == 65536 && ldpc::nb_ep_log2(65536) == 16, "chunk stride");
+}
+
+// The CLIs' codeword files (cli_common.h, decodeMinSum.cpp:136-143,193-212): the
+// reference's eof/rewind rule and the per-symbol conversion over odd inputs.
+static void one_codeword_file(const char *path, int N)
+{
+    const std::vector<std::string> lines = reference_codeword_lines(path);
+    CHECK(!lines.empty(), "%s: no codeword line", path);
+    std::vector<int8_t> c(N, 1);
+    std::ostringstream log;
+    for (const auto &l : lines) apply_codeword_line(l, N, c, log);
+    for (int i = 0; i < N; ++i) CHECK(c[i] == 1 || c[i] == -1, "%s: symbol %d not bipolar", path, i);
+    std::printf("%s: %zu codeword line(s), %zu bytes of invalid-symbol reports\n", path, lines.size(), log.str().size());
+}
+
+static void cli_inputs(const std::string &dir)
+{
+    const std::pair<const char *, std::string> files[] = {
+        {"cw_empty", ""},
+        {"cw_one_unterminated", "0101"},
+        {"cw_two_unterminated", "0101\n1100"},
+        {"cw_terminated", "0101\n1100\n"},
+        {"cw_junk", std::string("01\x00\xff\r\n\n\n2x", 11)},
+        {"cw_long", std::string(100000, '1') + "\n"},
+        {"cw_crlf", "0101\r\n1100\r\n"},
+    };
+    for (const auto &f : files) {
+        const std::string p = write_tmp(dir, f.first, f.second);
+        for (int N : {0, 1, 4, 7, 4096}) one_codeword_file(p.c_str(), N);
+    }
+    one_codeword_file((dir + "/does_not_exist.enc").c_str(), 8);   // unreadable: one empty line, all invalid
+    const std::pair<const char *, std::string> hdrs[] = {
+        {"hdr_empty", ""}, {"hdr_short", "8 4\n"}, {"hdr_text", "N M\n"}, {"hdr_ok", "8 4\n3 6\n"},
+        {"hdr_neg", "8 4\n-3 -6\n"}};
+    for (const auto &h : hdrs) {
+        const std::string p = write_tmp(dir, h.first, h.second);
+        int dv = -7, dc = -7;
+        alist_header(p.c_str(), dv, dc);
+        CHECK(dv != -7 && dc != -7, "%s: alist_header left its outputs unset", h.first);
+    }
+    int dv = -7, dc = -7;
+    alist_header((dir + "/does_not_exist.alist").c_str(), dv, dc);
+    CHECK(dv == 0 && dc == 0, "alist_header of a missing file");
+}
+
 int main(int argc, char **argv)
 {
-    for (int a = 1; a < argc; ++a) one_code(argv[a]);
+    std::string tmp = "/tmp";
+    std::vector<const char *> bin, nb, cw;
+    std::vector<const char *> *cur = &bin;
+    for (int a = 1; a < argc; ++a) {
+        const std::string s = argv[a];
+        if (s == "--nb") cur = &nb;
+        else if (s == "--cw") cur = &cw;
+        else if (s == "--tmp" && a + 1 < argc) tmp = argv[++a];
+        else cur->push_back(argv[a]);
+    }
+    for (const char *p : bin) one_code(p);
+    for (const char *p : nb) one_nb(p);
+    for (const char *p : cw) one_codeword_file(p, 1008);
+    nb_malformed(tmp);
+    cli_inputs(tmp);
     // malformed graphs: rejected with a message, never a crash
     {
         const int nn[2] = {1, 1}, nm[1] = {3};

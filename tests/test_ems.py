@@ -274,6 +274,54 @@ def test_ems_other_kernels_bit_exact(shape):
             assert np.array_equal(fr["iters"], its) and np.array_equal(fr["syndrome_fail"], sf)
 
 
+def _random_nb_code(N, M, dv, q, seed):
+    """A random column-regular GF(q) code (dv edges per symbol, rows as even as a
+    shuffled edge list makes them, no repeated edge), fast at any size (PEG is not)."""
+    codes = _codes()
+    rng = np.random.default_rng(seed)
+    while True:
+        sock = rng.permutation(np.repeat(np.arange(M), -(-N * dv // M)))[: N * dv].reshape(N, dv)
+        if all(len(set(r)) == dv for r in sock.tolist()):
+            break
+    cols = [[(int(c), int(rng.integers(1, q))) for c in sorted(r)] for r in sock.tolist()]
+    rows = [[] for _ in range(M)]
+    for v, r in enumerate(cols):
+        for c, h in r:
+            rows[c].append((v, h))
+    assert min(len(r) for r in rows) >= 2
+    return codes.NbParityCheck(N, M, q, rows, cols)
+
+
+@pytest.mark.gpu
+def test_ems_chunk_stride_65536_accepted_bit_exact():
+    """maxdc * M just above 32 768 (4 x 8 200 = 32 800 slots) rounds the chunk
+    stride up to 65 536; such a code is decoded (the 16-bit entries are the slot indices,
+    below 65 536), on the global-state kernel, equal to the oracle."""
+    native = _native()
+    H = _random_nb_code(16400, 8200, 2, 16, seed=65)
+    g = native.NbGraph.from_lists(H.N, H.M, H.q, H.cols, H.rows)
+    assert max(len(r) for r in H.rows) * H.M == 32800
+    ctx = native.NbContext(g, 0, 8)
+    assert ctx.kernel_info()["kernel"] == "ems_global"
+    A = O.NbCode(H)
+    y, n0 = _frames(H.N * 4, 3, 2.5, seed=65)
+    for T in (1, 4):
+        c = dict(nm=16, offset=0.0, early_stop=True)
+        d, fr, _ = ctx.decode(y, n0, native.EmsConfig(T=T, **c))
+        want, its, sf = A.decode(y, n0, T, **c)
+        assert int((d != want).sum()) == 0, T
+        assert np.array_equal(fr["iters"], its) and np.array_equal(fr["syndrome_fail"], sf)
+
+
+def test_nb_graph_above_the_16_bit_slot_bound_is_refused_at_context_creation_only():
+    """maxdc * M = 65 540 exceeds the 16-bit slot indices: the graph itself is valid
+    (host-side checks pass; the context refuses it with LDPC_ERR_UNSUPPORTED on a GPU box)."""
+    native = _native()
+    H = _random_nb_code(32770, 16385, 2, 16, seed=66)
+    g = native.NbGraph.from_lists(H.N, H.M, H.q, H.cols, H.rows)
+    assert (g.N, g.M) == (32770, 16385) and max(len(r) for r in H.rows) * H.M > 65535
+
+
 @pytest.mark.parametrize("name,q", [("q4.sp.9000.6000.4500.1.alist", 4), ("q8.sp.6000.4000.3000.1.alist", 8)])
 def test_reference_nb_codes_load_and_decode(name, q):
     """The reference's own GF(4) / GF(8) codes (SystemC/NB-LDPC/codes/GF4, GF8; fixtures
