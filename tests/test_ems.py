@@ -274,37 +274,47 @@ def test_ems_other_kernels_bit_exact(shape):
             assert np.array_equal(fr["iters"], its) and np.array_equal(fr["syndrome_fail"], sf)
 
 
-def _random_nb_code(N, M, dv, q, seed):
-    """A random column-regular GF(q) code (dv edges per symbol, rows as even as a
-    shuffled edge list makes them, no repeated edge), fast at any size (PEG is not)."""
+def _random_nb_code(col_deg, row_deg, q, seed):
+    """A random GF(q) code with the given column and row degrees (sum equal; no edge
+    twice), fast at any size (PEG is not)."""
     codes = _codes()
     rng = np.random.default_rng(seed)
-    while True:
-        sock = rng.permutation(np.repeat(np.arange(M), -(-N * dv // M)))[: N * dv].reshape(N, dv)
-        if all(len(set(r)) == dv for r in sock.tolist()):
+    col_deg, row_deg = list(col_deg), list(row_deg)
+    assert sum(col_deg) == sum(row_deg) and min(row_deg) >= 2
+    N, M = len(col_deg), len(row_deg)
+    rsock = np.repeat(np.arange(M), row_deg)
+    for _ in range(1000):
+        perm = rng.permutation(len(rsock))
+        cols, at = [], 0
+        for d in col_deg:
+            cols.append(sorted(int(r) for r in rsock[perm[at:at + d]]))
+            at += d
+        if all(len(set(c)) == len(c) for c in cols):
             break
-    cols = [[(int(c), int(rng.integers(1, q))) for c in sorted(r)] for r in sock.tolist()]
+    else:
+        raise RuntimeError("no simple graph found")
+    cols = [[(c, int(rng.integers(1, q))) for c in r] for r in cols]
     rows = [[] for _ in range(M)]
     for v, r in enumerate(cols):
         for c, h in r:
             rows[c].append((v, h))
-    assert min(len(r) for r in rows) >= 2
     return codes.NbParityCheck(N, M, q, rows, cols)
 
 
 @pytest.mark.gpu
 def test_ems_chunk_stride_65536_accepted_bit_exact():
-    """maxdc * M just above 32 768 (4 x 8 200 = 32 800 slots) rounds the chunk
-    stride up to 65 536; such a code is decoded (the 16-bit entries are the slot indices,
-    below 65 536), on the global-state kernel, equal to the oracle."""
+    """maxdc * M just above 32 768 (one row of degree 8 among 4 097: 32 776
+    slots) rounds the chunk stride up to 65 536 slots; such a code is decoded -- the
+    16-bit entries are the slot indices, below 65 536 -- on the global-state kernel
+    (4 MB of messages per codeword), equal to the oracle."""
     native = _native()
-    H = _random_nb_code(16400, 8200, 2, 16, seed=65)
+    H = _random_nb_code([3] * 4096 + [2] * 4, [8] + [3] * 4096, 16, seed=65)
+    assert max(len(r) for r in H.rows) * H.M == 32776
     g = native.NbGraph.from_lists(H.N, H.M, H.q, H.cols, H.rows)
-    assert max(len(r) for r in H.rows) * H.M == 32800
     ctx = native.NbContext(g, 0, 8)
     assert ctx.kernel_info()["kernel"] == "ems_global"
     A = O.NbCode(H)
-    y, n0 = _frames(H.N * 4, 3, 2.5, seed=65)
+    y, n0 = _frames(H.N * 4, 3, 2.2, seed=65)
     for T in (1, 4):
         c = dict(nm=16, offset=0.0, early_stop=True)
         d, fr, _ = ctx.decode(y, n0, native.EmsConfig(T=T, **c))
@@ -317,7 +327,7 @@ def test_nb_graph_above_the_16_bit_slot_bound_is_refused_at_context_creation_onl
     """maxdc * M = 65 540 exceeds the 16-bit slot indices: the graph itself is valid
     (host-side checks pass; the context refuses it with LDPC_ERR_UNSUPPORTED on a GPU box)."""
     native = _native()
-    H = _random_nb_code(32770, 16385, 2, 16, seed=66)
+    H = _random_nb_code([2] * 32770, [4] * 16385, 16, seed=66)
     g = native.NbGraph.from_lists(H.N, H.M, H.q, H.cols, H.rows)
     assert (g.N, g.M) == (32770, 16385) and max(len(r) for r in H.rows) * H.M > 65535
 
