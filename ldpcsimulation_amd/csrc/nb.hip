@@ -38,7 +38,8 @@ constexpr float kInf = __builtin_huge_valf();
 #endif
 // Timing-only ablations (wrong results; run with early stop off): 1 = no check
 // nodes, 2 = no symbol nodes, 3 = no per-iteration syndrome, 4 = check and symbol
-// nodes overlapped on two wave halves (one barrier interval per iteration).
+// nodes overlapped on two wave halves (one barrier interval per iteration; 5: the
+// symbol nodes on the older half; 6: as 4, symbol waves at raised priority).
 #ifndef LDPC_EMS_EXP
 #define LDPC_EMS_EXP 0
 #endif
@@ -502,17 +503,22 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
     const int cdir = (tid >> 5) & 1, cpr = (nt >> 6) * 32;
     const int cj0 = (tid >> 6) * 32 + (tid & 31);
     constexpr int KV = LDPC_EMS_VD > 0 ? LDPC_EMS_VD : 1;
-#if LDPC_EMS_EXP == 4
+#if LDPC_EMS_EXP >= 4 && LDPC_EMS_EXP <= 6
     // Timing experiment (results wrong by design; run without early stop): the
     // overlap a second codeword would allow, on one message array. Waves 0-7 run
-    // every check node, waves 8-15 every symbol node, concurrently in one barrier
-    // interval per iteration -- the cost of an iteration if the symbol phase of one
-    // codeword overlapped the check phase of another.
+    // every check node, waves 8-15 every symbol node (5: the other way round, so
+    // the latency-bound symbol waves are the older ones and win the oldest-first
+    // VALU arbitration; 6: as 4 with the symbol waves at s_setprio 3), concurrently in one barrier interval per iteration -- the
+    // cost of an iteration if the symbol phase of one codeword overlapped the check
+    // phase of another.
     while (it < a.T && (!a.early_stop || fail)) {
         const int half = nt / 2;
-        if (tid < half) {
+        const bool check_role = LDPC_EMS_EXP == 5 ? tid >= half : tid < half;
+        const int rt = tid < half ? tid : tid - half;
+        if (LDPC_EMS_EXP == 6 && !check_role) __builtin_amdgcn_s_setprio(3);
+        if (check_role) {
             const int cpr2 = (half >> 6) * 32;
-            int cj = (tid >> 6) * 32 + (tid & 31);
+            int cj = (rt >> 6) * 32 + (rt & 31);
             asm volatile("" : "+v"(cj));
             for (int j = cj; j < M; j += cpr2) {
                 switch (sc.cn_d[j]) {
@@ -523,14 +529,14 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
                 }
             }
         } else {
-            for (int v = tid - half; v < N; v += half) vn_lane<Q, MB, LDPC_EMS_VD, DC, GS>(ma, v, sc, lam, dec, false, synd);
+            for (int v = rt; v < N; v += half) vn_lane<Q, MB, LDPC_EMS_VD, DC, GS>(ma, v, sc, lam, dec, false, synd);
         }
         __syncthreads();
         fail = syndrome_read_reset(synd, (M + 3) / 4, red + 48);
         ++it;
     }
 #endif
-    while (LDPC_EMS_EXP != 4 && it < a.T && (!a.early_stop || fail)) {
+    while ((LDPC_EMS_EXP < 4 || LDPC_EMS_EXP > 6) && it < a.T && (!a.early_stop || fail)) {
         // ---- check nodes ----
         // the lane's first check, opaque per iteration: its message addresses are
         // recomputed here (a few VALU) instead of being hoisted out of the
