@@ -83,11 +83,11 @@ __device__ __forceinline__ double norm64(double m, double alpha, double rcp, dou
 #ifndef LDPC_FAST64_STORE_VALU
 #define LDPC_FAST64_STORE_VALU 3
 #endif
-// ACC (the ping-pong kernel): instead of a per-row premise compare and flag, the row
-// folds hi32(M2) into a per-thread sticky maximum pacc (one v_max_u32; M2 >= +0 or NaN,
-// so M2 < 2^1000 <=> hi32(M2) < kFast64MaxHi as u32, NaN and inf above it), and a tiny
-// minimum forces pacc to ~0; the caller flags the codeword once, after its last
-// iteration (the flag is only read then). Same set of re-decoded codewords.
+// ACC (the ping-pong kernel): instead of the f64 premise compare, the row folds
+// hi32(M2) into the maximum *pacc (one v_max_u32; M2 >= +0 or NaN, so M2 < 2^1000 <=>
+// hi32(M2) < kFast64MaxHi as u32, NaN and inf above it), and a tiny minimum forces
+// *pacc to ~0; the caller tests it (per row, or once per codeword when *pacc is a
+// sticky per-slot maximum: rows_pp.hip LDPC_PP_STICKY). Same set of re-decoded codewords.
 struct NoSink {
     __device__ __forceinline__ void operator()(int, const Pack<double, 1> &) const {}
 };

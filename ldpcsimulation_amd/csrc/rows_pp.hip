@@ -55,6 +55,13 @@ namespace {
 // a subtraction, 4 no c2v scatters, 5 gathers at lane-contiguous addresses (no
 // bank conflicts), 6 scatters at lane-contiguous addresses, 7 both 5 and 6.
 // LDPC_PP_BITDELAY: s_sleep units (64 cycles) the bit waves wait at an interval's start.
+// fp64 premise flag: 0 = each row's hi-word maximum (fast64.h ACC) tested by a
+// wave-uniform branch right after the row (no register lives across the step);
+// 1 = a per-slot sticky maximum tested once after the step's last iteration (two
+// VGPRs across the interval loop: the kernel setup then spills 16 B more per lane).
+#ifndef LDPC_PP_STICKY
+#define LDPC_PP_STICKY 0
+#endif
 #ifndef LDPC_PP_EXP
 #define LDPC_PP_EXP 0
 #endif
@@ -266,9 +273,8 @@ __device__ __forceinline__ void pp_account(const DecodeArgs &a, int *red, int gr
 // store(k, message) scatters the new message of edge k, called as each message is
 // formed, in per-edge order (LDPC_PP_STORE_ORDER), so the scatters overlap the selects
 // of the later edges (fp64: cn_fast64; fp32 pairs: cn_fast_pair).
-// fp64: the premise is folded into the slot's sticky hi-word maximum pacc (fast64.h ACC)
-// and checked once per codeword, after its last iteration (the slot flag is read only
-// then); the returned value is always true.
+// fp64: the premise is folded into the hi-word maximum *pacc (fast64.h ACC), tested by
+// the caller (LDPC_PP_STICKY); the returned value is always true.
 template <typename F, int DC, int VAR, bool FDIV, int C, int DCA, typename Store>
 __device__ __forceinline__ bool pp_check_node(const Pack<F, C> (&xin)[DCA], Pack<F, C> (&pv)[DCA], F alpha, F rcp,
                                               F delta, Store store, uint32_t *pacc)
@@ -352,7 +358,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
     const int nsteps = (a.batch + 2 * C - 1) / (2 * C);
     PP_STAMP_DECL;
     for (int grp = blockIdx.x; grp < nsteps; grp += gridDim.x) {
-        [[maybe_unused]] uint32_t pacc[2] = {0u, 0u};   // fp64: per-slot sticky premise maximum (pp_check_node)
+        [[maybe_unused]] uint32_t pacc[2] = {0u, 0u};   // fp64, LDPC_PP_STICKY: per-slot premise maximum
         int unc[2 * C];
 #pragma unroll
         for (int q = 0; q < 2 * C; ++q) unc[q] = 0;
@@ -466,7 +472,14 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                                 store(k, prev[X][r][k]);
                             }
                         } else {
-                            ok = pp_check_node<F, DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta, store, &pacc[X]);
+                            [[maybe_unused]] uint32_t pa = 0;
+                            ok = pp_check_node<F, DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta, store,
+                                                                  LDPC_PP_STICKY ? &pacc[X] : &pa);
+                            if constexpr (F64 && !LDPC_PP_STICKY) {
+                                // rare: M2 >= 2^1000 (inf, NaN) or a tiny minimum in this row
+                                if (__builtin_amdgcn_ballot_w64(pa >= kFast64MaxHi))
+                                    if (pa >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[X] = 1;
+                            }
                         }
                         if (!ok && deg[r] > 0 && LDPC_PP_EXP == 0) s.red[X] = 1;   // experiments: never re-decode
                         if (R > 1 && LDPC_PP_ROWFENCE) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
@@ -484,7 +497,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
             interval(std::integral_constant<int, 0>(), false, true);
             PP_BARRIER();   // | -- | bit(1,T-1) |
         }
-        if constexpr (F64 && R > 0) {   // the premise of every iteration of the step (fast64.h ACC)
+        if constexpr (F64 && R > 0 && LDPC_PP_STICKY) {   // the premise of every iteration of the step
             if (pacc[0] >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[0] = 1;
             if (pacc[1] >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[1] = 1;
         }

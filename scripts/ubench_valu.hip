@@ -3,7 +3,7 @@
 // nothing folds); the grid fills every SIMD with W waves. Reports cycles per
 // wave-instruction per SIMD (clock from the -c argument, default 2.4 GHz is
 // NOT assumed: s_memtime is read inside the kernel).
-//   hipcc --offload-arch=gfx950 -O3 -o ubench_valu scripts/ubench_valu.hip
+//   hipcc --offload-arch=gfx950 -O3 -o ab/ubench_valu scripts/ubench_valu.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -57,18 +57,16 @@ __global__ __launch_bounds__(256) void k_cmp(unsigned long long *cyc, double *si
     unsigned long long m = 0;
     for (int i = 0; i < ITER; ++i) {
         unsigned long long c0, c1, c2, c3, c4, c5, c6, c7;
-        if constexpr (OP == 0)
-            asm volatile("v_cmp_le_f64_e64 %0, %8, %9\n\tv_cmp_le_f64_e64 %1, %8, %9\n\tv_cmp_le_f64_e64 %2, %8, %9\n\t"
-                         "v_cmp_le_f64_e64 %3, %8, %9\n\tv_cmp_le_f64_e64 %4, %8, %9\n\tv_cmp_le_f64_e64 %5, %8, %9\n\t"
-                         "v_cmp_le_f64_e64 %6, %8, %9\n\tv_cmp_le_f64_e64 %7, %8, %9"
-                         : "=s"(c0), "=s"(c1), "=s"(c2), "=s"(c3), "=s"(c4), "=s"(c5), "=s"(c6), "=s"(c7)
-                         : "v"(a), "v"(b));
-        else
-            asm volatile("v_cmp_le_u64_e64 %0, %8, %9\n\tv_cmp_le_u64_e64 %1, %8, %9\n\tv_cmp_le_u64_e64 %2, %8, %9\n\t"
-                         "v_cmp_le_u64_e64 %3, %8, %9\n\tv_cmp_le_u64_e64 %4, %8, %9\n\tv_cmp_le_u64_e64 %5, %8, %9\n\t"
-                         "v_cmp_le_u64_e64 %6, %8, %9\n\tv_cmp_le_u64_e64 %7, %8, %9"
-                         : "=s"(c0), "=s"(c1), "=s"(c2), "=s"(c3), "=s"(c4), "=s"(c5), "=s"(c6), "=s"(c7)
-                         : "v"(a), "v"(b));
+#define CMP8(INS, A)                                                                                   \
+    asm volatile(INS " %0, " A ", %9\n\t" INS " %1, " A ", %9\n\t" INS " %2, " A ", %9\n\t" INS " %3, " A        \
+                 ", %9\n\t" INS " %4, " A ", %9\n\t" INS " %5, " A ", %9\n\t" INS " %6, " A ", %9\n\t" INS " %7, " A \
+                 ", %9"                                                                                       \
+                 : "=s"(c0), "=s"(c1), "=s"(c2), "=s"(c3), "=s"(c4), "=s"(c5), "=s"(c6), "=s"(c7)            \
+                 : "v"(a), "v"(b))
+        if constexpr (OP == 0) CMP8("v_cmp_le_f64_e64", "%8");
+        if constexpr (OP == 1) CMP8("v_cmp_le_u64_e64", "%8");
+        if constexpr (OP == 2) CMP8("v_cmp_eq_f64_e64", "|%8|");   // the check node's argmin mask
+        if constexpr (OP == 3) CMP8("v_cmp_eq_u64_e64", "%8");
         m ^= c0 ^ c1 ^ c2 ^ c3 ^ c4 ^ c5 ^ c6 ^ c7;
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -124,6 +122,8 @@ int main()
         run("v_sub_u32", k_bench<7>, w);
         run("v_cmp_le_f64", k_cmp<0>, w);
         run("v_cmp_le_u64", k_cmp<1>, w);
+        run("v_cmp_eq_f64|a|", k_cmp<2>, w);
+        run("v_cmp_eq_u64", k_cmp<3>, w);
     }
     return 0;
 }
