@@ -80,6 +80,9 @@ __device__ __forceinline__ double norm64(double m, double alpha, double rcp, dou
 // new c2v. Returns false when the premise may fail for the next iteration (or
 // failed for this one's division).
 // VALU instructions the scheduler places ahead of each edge's store (ORDER).
+#ifndef LDPC_FAST64_CMPFIRST
+#define LDPC_FAST64_CMPFIRST 0
+#endif
 #ifndef LDPC_FAST64_STORE_VALU
 #define LDPC_FAST64_STORE_VALU 3
 #endif
@@ -149,10 +152,19 @@ __device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DCA], Pac
     uint32_t s1 = hi32(M1) ^ (par & mk1), s2 = hi32(M2) ^ (par & mk2);
     asm("" : "+v"(s1), "+v"(s2));   // keep the parity out of the per-edge select
     const uint32_t l1 = lo32(M1), l2 = lo32(M2);
+    // |v2c_k| == min1 as one v_cmp_eq_f64 with the abs source modifier, used as the select mask;
+    // CMPFIRST: every edge's mask formed ahead of the per-edge selects and stores (SGPR pairs),
+    // so no select waits on the compare just issued (the f64-compare -> mask-read wait states)
+    [[maybe_unused]] uint64_t eqm[DC];
+    if constexpr (LDPC_FAST64_CMPFIRST) {
+#pragma unroll
+        for (int k = 0; k < DC; ++k) eqm[k] = __builtin_amdgcn_fcmp(__builtin_fabs(x[k]), mn1, 1);
+        if constexpr (ORDER) __builtin_amdgcn_sched_group_barrier(0x2, DC, 0);
+    }
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        // |v2c_k| == min1 as one v_cmp_eq_f64 with the abs source modifier, used as the select mask
-        const bool eq = __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_fcmp(__builtin_fabs(x[k]), mn1, 1));
+        const bool eq = __builtin_amdgcn_inverse_ballot_w64(
+            LDPC_FAST64_CMPFIRST ? eqm[k] : __builtin_amdgcn_fcmp(__builtin_fabs(x[k]), mn1, 1));
         const uint32_t h = eq ? s2 : s1, l = eq ? l2 : l1;
         const uint32_t m = (VAR == V_OMS) ? (eq ? mk2 : mk1) : SIGN;
         pv[k].v[0] = mkd(l, __builtin_amdgcn_bitop3_b32(h, hi32(x[k]), m, 0x78));   // h ^ (v2c_k & m)

@@ -477,8 +477,10 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                                                                   LDPC_PP_STICKY ? &pacc[X] : &pa);
                             if constexpr (F64 && !LDPC_PP_STICKY) {
                                 // rare: M2 >= 2^1000 (inf, NaN) or a tiny minimum in this row
-                                if (__builtin_amdgcn_ballot_w64(pa >= kFast64MaxHi))
+                                if (__builtin_amdgcn_ballot_w64(pa >= kFast64MaxHi)) {
+                                    asm volatile("" : "+v"(pa));   // a side effect: stays a skipped branch
                                     if (pa >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[X] = 1;
+                                }
                             }
                         }
                         if (!ok && deg[r] > 0 && LDPC_PP_EXP == 0) s.red[X] = 1;   // experiments: never re-decode
