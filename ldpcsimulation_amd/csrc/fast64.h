@@ -136,7 +136,7 @@ __device__ __forceinline__ bool cn_fast64(const Pack<double, 1> (&xin)[DCA], Pac
 #endif
             if constexpr (ACC) {
                 uint32_t t = *pacc;
-                asm volatile("" : "+v"(t));   // a side effect: the rare path stays a branch (not if-converted)
+                asm volatile(";");   // a side effect: the rare path stays a branch (not if-converted)
                 if ((mn1 > 0.0 && mn1 < kFast64Tiny) | (mn2 > 0.0 && mn2 < kFast64Tiny)) t = ~0u;
                 *pacc = t;
             } else {

@@ -478,7 +478,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                             if constexpr (F64 && !LDPC_PP_STICKY) {
                                 // rare: M2 >= 2^1000 (inf, NaN) or a tiny minimum in this row
                                 if (__builtin_amdgcn_ballot_w64(pa >= kFast64MaxHi)) {
-                                    asm volatile("" : "+v"(pa));   // a side effect: stays a skipped branch
+                                    asm volatile(";");   // a side effect: stays a skipped branch
                                     if (pa >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[X] = 1;
                                 }
                             }
