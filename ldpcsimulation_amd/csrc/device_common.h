@@ -50,8 +50,19 @@ __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, float &n0, 
     n0 = rad * c;
     n1 = rad * s;
 }
+// LDPC_BM32 (experiment): the fp64 channel's normals from the fp32 transform, widened.
+#ifndef LDPC_BM32
+#define LDPC_BM32 0
+#endif
 __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, double &n0, double &n1)
 {
+    if constexpr (LDPC_BM32) {
+        float f0, f1;
+        box_muller(ua, ur, f0, f1);
+        n0 = (double)f0;
+        n1 = (double)f1;
+        return;
+    }
     const double a = ((double)ua + 0.5) * 2.3283064365386963e-10;
     const double r = ((double)ur + 0.5) * 2.3283064365386963e-10;
     const double rad = sqrt(-2.0 * log(r));

@@ -62,6 +62,11 @@ namespace {
 #ifndef LDPC_PP_STICKY
 #define LDPC_PP_STICKY 0
 #endif
+// Timing ablations of the per-step work (results wrong by design): 1 no channel
+// generation, 2 no syndrome / decisions, 4 no block reduction.
+#ifndef LDPC_PP_TAILEXP
+#define LDPC_PP_TAILEXP 0
+#endif
 #ifndef LDPC_PP_EXP
 #define LDPC_PP_EXP 0
 #endif
@@ -236,15 +241,49 @@ __device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots<Pa
     }
 }
 
+// A wave's sum of per-lane counts 0..7, bit-sliced: three ballots and popcounts on the
+// scalar unit instead of a cross-lane shuffle tree.
+__device__ __forceinline__ int wave_sum3(int x)
+{
+    return __builtin_popcountll(__builtin_amdgcn_ballot_w64((x & 1) != 0)) +
+           2 * __builtin_popcountll(__builtin_amdgcn_ballot_w64((x & 2) != 0)) +
+           4 * __builtin_popcountll(__builtin_amdgcn_ballot_w64((x & 4) != 0));
+}
+
 // Block sums of the step's (bit errors, uncoded errors, syndrome) per codeword and
 // the per-codeword accounting (:270-288, :382-393) by thread 0; the codewords of a
-// slot whose premise failed go to the re-decode list instead.
-template <int C>
+// slot whose premise failed go to the re-decode list instead. Per lane the counts are
+// small -- a bit-role lane holds CPT = 4 bit slots and one Philox group of each
+// codeword (N <= 2048, rows_pp_supported), so its bit and uncoded errors are <= 4; a
+// check-role lane holds the 0/1 syndrome of its rows -- so each wave sums them by
+// ballots (wave_sum3; the syndrome is an OR) and lane 0 adds the wave's totals into
+// red[kPPRedSums ...] with LDS atomics: one barrier, and only thread 0 reads the totals
+// (it clears them for the next step).
+template <int C, bool HB>
 __device__ __forceinline__ void pp_account(const DecodeArgs &a, int *red, int grp, int (&sums)[6 * C], unsigned *redo,
                                            unsigned long long *acc)
 {
-    block_sum_n<6 * C>(sums, red + kPPRedSums);
+    int *tot = red + kPPRedSums;
+    const bool lane0 = (threadIdx.x & 63) == 0;
+    if (!(LDPC_PP_TAILEXP & 4)) {
+#pragma unroll
+        for (int q = 0; q < 2 * C; ++q) {
+            if constexpr (HB) {
+                const int w = wave_sum3(sums[3 * q]), u = wave_sum3(sums[3 * q + 1]);
+                if (lane0 && w) atomicAdd(&tot[3 * q], w);
+                if (lane0 && u) atomicAdd(&tot[3 * q + 1], u);
+            } else {
+                if (__builtin_amdgcn_ballot_w64(sums[3 * q + 2] != 0) && lane0) atomicAdd(&tot[3 * q + 2], 1);
+            }
+        }
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < 6 * C; ++v) {
+            sums[v] = tot[v];
+            tot[v] = 0;
+        }
         const int fl[2] = {red[0], red[1]};
         red[0] = red[1] = 0;   // read once per step; raised again only after the next B1
 #pragma unroll
@@ -362,7 +401,15 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
         int unc[2 * C];
 #pragma unroll
         for (int q = 0; q < 2 * C; ++q) unc[q] = 0;
-        if constexpr (HB) pp_channel<F, SRC>(a, s, N, grp, unc, bt, kPPRole);
+        if constexpr (HB) {
+            if (!(LDPC_PP_TAILEXP & 1)) {
+                pp_channel<F, SRC>(a, s, N, grp, unc, bt, kPPRole);
+            } else {   // timing only: a constant channel
+                for (int q = 0; q < 2 * C; ++q) unc[q] = 0;
+                for (int v = bt; v < N; v += kPPRole)
+                    for (int c = 0; c < C; ++c) s.app[0][v].v[c] = s.app[1][v].v[c] = F(1);
+            }
+        }
         __syncthreads();   // B1: channel staged
         [[maybe_unused]] P yq[2][CPT];
         if constexpr (R > 0) {
@@ -504,6 +551,11 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
             if (pacc[1] >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[1] = 1;
         }
 
+        if (LDPC_PP_TAILEXP & 2) {   // timing only: no syndrome, decisions or error weights
+            int sums[6 * C] = {};
+            pp_account<C, HB>(a, s.red, grp, sums, redo, acc);
+            continue;
+        }
         // syndrome (rows; padding edges read +inf: parity 0; rows past M skipped) and
         // decisions / error weight (bit slots; :270, :382-393) of the step's codewords
         int sums[6 * C];
@@ -549,7 +601,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                 }
             }
         }
-        pp_account<C>(a, s.red, grp, sums, redo, acc);
+        pp_account<C, HB>(a, s.red, grp, sums, redo, acc);
     }
     PP_STAMP_OUT()
 }
@@ -578,6 +630,8 @@ __global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph 
         s.red[0] = s.red[1] = 0;
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
+#pragma unroll
+        for (int v = 0; v < 3 * kPPMaxCw; ++v) s.red[kPPRedSums + v] = 0;   // pp_account's totals
     }
     // the split is wave-uniform (an SGPR branch), so every wave meets every barrier
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
