@@ -8,30 +8,27 @@ namespace ldpc {
 
 // ---------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al. SC'11) + Box-Muller: 4 normals per call.
-// LDPC_PHILOX_MAD64: the two 32x32->64 products of a round as v_mad_u64_u32
-// (same values either way). On in gdbf.hip, where Philox runs every iteration;
-// off elsewhere: in the fp64 row kernel, which draws once per codeword, the
-// 64-bit form costs 2.5 % through register allocation (16.10 vs 16.52 ms,
-// 3 interleaved rounds).
+// MAD64: the two 32x32->64 products of a round as v_mad_u64_u32 (same values
+// either way; 20 instead of 40 quarter-rate multiplies per call). Used by gdbf.hip,
+// where Philox runs every iteration, and by the ping-pong kernel's channel (12.54-12.58
+// vs 12.60-12.66 ms); off in the fp64 one-codeword row kernel, where the 64-bit form
+// costs 2.5 % through register allocation (16.10 vs 16.52 ms, 3 interleaved rounds).
 // ---------------------------------------------------------------------
-#ifndef LDPC_PHILOX_MAD64
-#define LDPC_PHILOX_MAD64 0
-#endif
+template <bool MAD64 = false>
 __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                               uint32_t k0, uint32_t k1, uint32_t out[4])
 {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-#if LDPC_PHILOX_MAD64
-        // one v_mad_u64_u32 per product (lo and hi together) instead of a
-        // v_mul_lo_u32 + v_mul_hi_u32 pair: 20 quarter-rate multiplies per call, not 40
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
-        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-#else
-        const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-        const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-#endif
+        uint32_t lo0, hi0, lo1, hi1;
+        if constexpr (MAD64) {
+            const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+            lo0 = (uint32_t)p0; hi0 = (uint32_t)(p0 >> 32);
+            lo1 = (uint32_t)p1; hi1 = (uint32_t)(p1 >> 32);
+        } else {
+            lo0 = 0xD2511F53u * c0; hi0 = __umulhi(0xD2511F53u, c0);
+            lo1 = 0xCD9E8D57u * c2; hi1 = __umulhi(0xCD9E8D57u, c2);
+        }
         const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
@@ -50,26 +47,31 @@ __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, float &n0, 
     n0 = rad * c;
     n1 = rad * s;
 }
-// LDPC_BM32 (experiment): the fp64 channel's normals from the fp32 transform, widened.
-#ifndef LDPC_BM32
-#define LDPC_BM32 0
+// The fp64 channel's normals: the fp32 transform above, widened to double (SURVEY
+// §8 a2: Philox4x32-10 + Box-Muller in fp32). The decoders compute in fp64 on the
+// widened samples y = c (1 + sigma n) exactly as on any given y; only the noise
+// generator's own precision is fp32 (fp64 log / sqrt / sincospi cost 2.6 % of the fp64
+// headline launch: 12.27-12.31 vs 12.60-12.66 ms). LDPC_BM64=1 (variant builds) keeps
+// the fp64 transform.
+#ifndef LDPC_BM64
+#define LDPC_BM64 0
 #endif
 __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, double &n0, double &n1)
 {
-    if constexpr (LDPC_BM32) {
+    if constexpr (!LDPC_BM64) {
         float f0, f1;
         box_muller(ua, ur, f0, f1);
         n0 = (double)f0;
         n1 = (double)f1;
-        return;
+    } else {
+        const double a = ((double)ua + 0.5) * 2.3283064365386963e-10;
+        const double r = ((double)ur + 0.5) * 2.3283064365386963e-10;
+        const double rad = sqrt(-2.0 * log(r));
+        double s, c;
+        sincospi(2.0 * a, &s, &c);
+        n0 = rad * c;
+        n1 = rad * s;
     }
-    const double a = ((double)ua + 0.5) * 2.3283064365386963e-10;
-    const double r = ((double)ur + 0.5) * 2.3283064365386963e-10;
-    const double rad = sqrt(-2.0 * log(r));
-    double s, c;
-    sincospi(2.0 * a, &s, &c);
-    n0 = rad * c;
-    n1 = rad * s;
 }
 
 // Sum over the workgroup (64-wide waves, <= 16 waves).

@@ -22,7 +22,6 @@
 // verification, given by the caller as pert[frame][it][bit].
 // Compiled with -ffp-contract=off: E is accumulated with the reference's
 // operation order, so fp64 decisions equal the reference's for the same noise.
-#define LDPC_PHILOX_MAD64 1   // Philox every iteration: 20 instead of 40 quarter-rate multiplies
 #include "gdbf.h"
 #include "device_common.h"
 #include "minsum_common.h"
@@ -139,7 +138,7 @@ __device__ __forceinline__ void gdbf_codeword(const GdbfArgs &a, const DevGraph 
             for (int q = 0; q < 4; ++q) yv[q] = (g4 * 4 + q < N) ? y[g4 * 4 + q] : F(1);
         } else {
             uint32_t u[4];
-            philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+            philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
             F n[4];
             box_muller(u[0], u[1], n[0], n[1]);
             box_muller(u[2], u[3], n[2], n[3]);
@@ -203,7 +202,7 @@ __device__ __forceinline__ void gdbf_codeword(const GdbfArgs &a, const DevGraph 
                     for (int q = 0; q < 4; ++q) pv[q] = (g4 * 4 + q < N) ? pr[g4 * 4 + q] : F(0);
                 } else {
                     uint32_t u[4];
-                    philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32),
+                    philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32),
                                   (a.stream_id & 0xFFFFFu) | ((uint32_t)(it + 1) << 20), k0, k1, u);
                     if (qprob) {
 #pragma unroll
@@ -503,7 +502,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
                 for (int q = 0; q < BPT; ++q) yv[q] = (v0 + q < N) ? y[v0 + q] : F(1);
             } else {
                 uint32_t u[4];
-                philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
                 F n[4];
                 box_muller(u[0], u[1], n[0], n[1]);
                 box_muller(u[2], u[3], n[2], n[3]);
@@ -570,7 +569,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
                     for (int q = 0; q < BPT; ++q) pv[q] = (v0 + q < N) ? pr[v0 + q] : F(0);
                 } else {
                     uint32_t u[4];
-                    philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32),
+                    philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32),
                                   (a.stream_id & 0xFFFFFu) | ((uint32_t)(it + 1) << 20), k0, k1, u);
                     float n[4];
                     pert_normals(u[0], u[1], n[0], n[1]);

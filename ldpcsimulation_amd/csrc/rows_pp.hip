@@ -211,7 +211,7 @@ __device__ __forceinline__ void pp_channel(const DecodeArgs &a, const PPSlots<Pa
         } else {
             cvec = a.cw_table ? a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N : nullptr;
             uint32_t u[4];
-            philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, (uint32_t)a.seed,
+            philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, (uint32_t)a.seed,
                           (uint32_t)(a.seed >> 32), u);
             F n[4];
             box_muller(u[0], u[1], n[0], n[1]);
