@@ -74,22 +74,8 @@ __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, double &n0,
     }
 }
 
-// Sum over the workgroup (64-wide waves, <= 16 waves).
-__device__ __forceinline__ int block_sum(int x, int *red)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    __syncthreads();
-    if (l == 0) red[w] = x;
-    __syncthreads();
-    int s = 0;
-    const int nw = (blockDim.x + 63) >> 6;
-    for (int i = 0; i < nw; ++i) s += red[i];
-    return s;
-}
-
 // Sums of NV values over the workgroup with one barrier pair; red holds 16*NV ints.
+// The totals are valid in thread 0 only.
 template <int NV>
 __device__ __forceinline__ void block_sum_n(int (&x)[NV], int *red)
 {
@@ -103,11 +89,15 @@ __device__ __forceinline__ void block_sum_n(int (&x)[NV], int *red)
 #pragma unroll
         for (int v = 0; v < NV; ++v) red[w * NV + v] = x[v];
     __syncthreads();
+    // the block totals are thread 0's (every caller reads them there): the other
+    // threads skip the 16 x NV partial reads
+    if (threadIdx.x == 0) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-        int t = 0;
-        for (int i = 0; i < nw; ++i) t += red[i * NV + v];
-        x[v] = t;
+        for (int v = 0; v < NV; ++v) {
+            int t = 0;
+            for (int i = 0; i < nw; ++i) t += red[i * NV + v];
+            x[v] = t;
+        }
     }
 }
 

@@ -170,9 +170,13 @@ __device__ __forceinline__ void decode_codeword(const DecodeArgs &a, const DevGr
         for (int k = 0; k < deg; ++k) par ^= (app[rc[k]] > F(0)) ? 0 : 1;
         synd |= par;
     }
-    w = block_sum(w, red);
-    unc = block_sum(unc, red);
-    synd = block_sum(synd, red);
+    {
+        int sums[3] = {w, unc, synd};
+        block_sum_n<3>(sums, red);
+        w = sums[0];
+        unc = sums[1];
+        synd = sums[2];
+    }
     if (tid == 0) {
         atomicAdd(&a.counts[0], (unsigned long long)w);
         atomicAdd(&a.counts[1], (unsigned long long)(w > 0));
