@@ -666,8 +666,10 @@ int rows_pp_lds_bytes(const DevGraph &g, const RowSched &rs)
 
 bool rows_pp_supported(const DevGraph &g, const RowSched &rs)
 {
+    // N <= 4 * kPPRole: a bit-role lane then holds <= 4 bits and one Philox group per
+    // codeword, the bound pp_account's ballot-sliced wave sums rely on
     return rs.threads == kPPRole && rs.rpt == 2 && rs.cpt == 4 && rs.dc == 8 && (rs.dc_low == 0 || rs.dc_low == 7) &&
-           g.N + 3 <= 0xffff && rows_pp_lds_bytes(g, rs) <= 160 * 1024;
+           g.N <= 4 * kPPRole && g.N + 3 <= 0xffff && rows_pp_lds_bytes(g, rs) <= 160 * 1024;
 }
 
 template <typename F, int SRC, int VAR, bool FDIV>
