@@ -33,6 +33,8 @@ struct NbArgs {
     float *y_out;                 // SRC_PHILOX: generated samples [batch][N * m] or null
     int4 *frame_res;              // [batch] {bit_err, uncoded, syndrome_fail, iterations} or null
     unsigned long long *counts;   // [7] bit, frame, uncoded, frames, iters, syndrome_fail, symbol errors
+    unsigned *ticket;             // codewords past the first grid's are handed out by this counter
+                                  // (nb_launch zeroes it): early stop makes codewords unequal
 };
 
 struct NbChoice {

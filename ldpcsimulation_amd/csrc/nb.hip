@@ -40,6 +40,10 @@ constexpr float kInf = __builtin_huge_valf();
 // nodes, 2 = no symbol nodes, 3 = no per-iteration syndrome, 4 = check and symbol
 // nodes overlapped on two wave halves (one barrier interval per iteration; 5: the
 // symbol nodes on the older half; 6: as 4, symbol waves at raised priority).
+// 1: codewords handed out by a global ticket counter after the first grid (0: fixed stride).
+#ifndef LDPC_EMS_TICKETS
+#define LDPC_EMS_TICKETS 1
+#endif
 #ifndef LDPC_EMS_EXP
 #define LDPC_EMS_EXP 0
 #endif
@@ -623,7 +627,7 @@ __host__ __device__ inline size_t aux_bytes(const NbDevGraph &g)
 {
     return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.M) +
            align16((size_t)g.N * 4) + align16((size_t)g.E * 2) + align16((size_t)g.E) +
-           align16((size_t)(g.M + 3) / 4 * 4) + (16 * 3 + 16) * 4;
+           align16((size_t)(g.M + 3) / 4 * 4) + (16 * 3 + 16 + 4) * 4;
 }
 
 template <int Q, int MB, int DC, int SRC, bool GSTATE, int THREADS>
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
     p += align16((size_t)g.E);
     uint32_t *synd = reinterpret_cast<uint32_t *>(p);   // check j: byte j & 3 of word j >> 2
     p += align16((size_t)(g.M + 3) / 4 * 4);
-    int *red = reinterpret_cast<int *>(p);                // block_sum_n scratch, then the wave flags
+    int *red = reinterpret_cast<int *>(p);   // block_sum_n scratch [0, 48), wave flags [48, 64), the ticket [64]
     for (int w = threadIdx.x; w < (g.M + 3) / 4; w += blockDim.x) synd[w] = 0u;
     for (int j = threadIdx.x; j < g.M; j += blockDim.x) cn_d[j] = (uint8_t)(g.row_ptr[j + 1] - g.row_ptr[j]);
     for (int v = threadIdx.x; v < g.N; v += blockDim.x)
@@ -666,8 +670,24 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
     __syncthreads();
     const NbSched sc{Ep, g.M, nb_ep_log2(Ep) + 4, cn_d, vn, vslot, vh};
     EmsStamps st;
-    for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
+    // Codewords: blockIdx.x first, then tickets from a.ticket (a global counter), so a
+    // block whose codewords stopped early takes more -- with early stop the iterations per
+    // codeword vary, and a fixed stride left the launch to the block with the most. Thread
+    // 0 draws the next ticket while the current codeword decodes (its latency hidden) and
+    // publishes it in red[64] after the codeword (whose barriers separate the reads).
+    [[maybe_unused]] unsigned nxt = 0;
+    if (LDPC_EMS_TICKETS && threadIdx.x == 0) nxt = gridDim.x + atomicAdd(a.ticket, 1u);
+    for (int b = blockIdx.x; b < a.batch;) {
         ems_codeword<Q, MB, DC, SRC, GSTATE>(a, g, b, msg, lam, dec, sc, red, synd, st);
+        if (LDPC_EMS_TICKETS) {
+            if (threadIdx.x == 0) red[64] = (int)nxt;
+            __syncthreads();
+            b = red[64];
+            if (threadIdx.x == 0 && b < a.batch) nxt = gridDim.x + atomicAdd(a.ticket, 1u);
+        } else {
+            b += gridDim.x;
+        }
+    }
 #ifdef LDPC_EMS_STAMPS
     if ((threadIdx.x & 63) == 0 && blockIdx.x < kEmsStampBlocks && (threadIdx.x >> 6) < 16)
         for (int k = 0; k < 8; ++k) g_ems_stamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + k] = st.v[k];
@@ -764,6 +784,11 @@ hipError_t nb_launch(const NbDevGraph &g, const NbArgs &a, const NbChoice &ch, v
         if (e != hipSuccess) return e;
     }
 #endif
+    if (LDPC_EMS_TICKETS) {
+        if (!a.ticket) return hipErrorInvalidValue;
+        const hipError_t e = hipMemsetAsync(a.ticket, 0, sizeof(unsigned), s);
+        if (e != hipSuccess) return e;
+    }
     const hipError_t err =
         ch.dc == 4 ? launch_dc<4>(g, a, ch, scratch, grid, s) : launch_dc<8>(g, a, ch, scratch, grid, s);
 #ifdef LDPC_EMS_STAMPS

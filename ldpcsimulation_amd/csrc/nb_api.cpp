@@ -301,6 +301,7 @@ static void fill_cfg(ldpc::NbArgs &a, ldpc_nb_ctx *c, const ldpc_ems_cfg *cfg, i
     a.early_stop = cfg->early_stop ? 1 : 0;
     a.offset = (float)cfg->offset;
     a.counts = (unsigned long long *)c->counts.p;
+    a.ticket = reinterpret_cast<unsigned *>((unsigned long long *)c->counts.p + 7);   // the 8th word of counts
 }
 
 int ldpc_ems_decode_batch(ldpc_nb_ctx *c, const float *y, int batch, double n0, const ldpc_ems_cfg *cfg,
