@@ -1103,6 +1103,7 @@ static void gdbf_fill(ldpc::GdbfArgs &a, ldpc_ctx *c, const ldpc_gdbf_cfg *cfg, 
     a.qsigma = cfg->qsigma;
     a.counts = (unsigned long long *)c->counts.p;
     a.hist = (unsigned long long *)c->hist.p;
+    a.ticket = reinterpret_cast<unsigned *>((unsigned long long *)c->counts.p + 7);   // the 8th word of counts
 }
 
 static int gdbf_run(ldpc_ctx *c, const ldpc::GdbfArgs &a, bool f64)

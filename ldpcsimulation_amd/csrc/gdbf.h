@@ -26,6 +26,8 @@ struct GdbfArgs {
     int4 *frame_res;                // [batch] {bit_err, uncoded, syndrome_fail, iterations} or null
     unsigned long long *counts;     // [6] accumulated (iters = sum of iterations run)
     unsigned long long *hist;       // [N] error-weight histogram
+    unsigned *ticket;               // gdbf_rows: codewords past the first grid's are handed out by
+                                    // this counter (gdbf_launch zeroes it): early stop makes them unequal
 };
 
 struct GdbfChoice {

@@ -404,6 +404,10 @@ static GdbfRowsLayout gdbf_rows_layout(int N, int M, int fsz)
 // 1: the perturbations are drawn between the row gathers and their use; 0 (default):
 // after the check phase's barrier -- fewer live registers, measured 21.4 vs 22.8 ms
 // (fp32) and 28.2 vs 28.7 ms (fp64), 2 interleaved rounds
+// 1: gdbf_rows hands out codewords past the first grid by a global ticket counter.
+#ifndef LDPC_GDBF_TICKETS
+#define LDPC_GDBF_TICKETS 1
+#endif
 #ifndef LDPC_GDBF_HOIST
 #define LDPC_GDBF_HOIST 0
 #endif
@@ -420,7 +424,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
 {
     constexpr int DC = 8, BPT = 4, RPT = 2;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ int red[16 * 4];
+    __shared__ int red[16 * 4 + 1];                    // block sums; [64]: the next codeword
     uint8_t *dl = smem;                                // 1 where d = -1
     F *sl = reinterpret_cast<F *>(smem + soff);        // w * s_j, the term a bit adds for check j
     volatile int *fl = reinterpret_cast<int *>(smem + floff);
@@ -475,7 +479,12 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
     const F w = (F)a.w, lambda = (F)a.lambda, nsig = (F)a.noise_sigma;
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
 
-    for (int b = blockIdx.x; b < a.batch; b += gridDim.x) {
+    // Codewords: blockIdx.x first, then tickets from a.ticket, so that a block whose
+    // codewords stopped early takes more (the iterations per codeword run from a few to
+    // T); thread 0 draws the next ticket while the current codeword decodes.
+    [[maybe_unused]] unsigned nxt = 0;
+    if (LDPC_GDBF_TICKETS && tid == 0) nxt = gridDim.x + atomicAdd(a.ticket, 1u);
+    for (int b = blockIdx.x; b < a.batch;) {
         const uint64_t cw = a.first_cw + (uint64_t)b;
         const int8_t *cvec = nullptr;
         if (SRC == SRC_GIVEN) {
@@ -671,8 +680,15 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
             atomicAdd(&a.counts[5], (unsigned long long)sf);
             if (sums[0] > 0 && a.hist) atomicAdd(&a.hist[sums[0] - 1], 1ull);
             if (a.frame_res) a.frame_res[b] = make_int4(sums[0], sums[1], sf, it);
+            if (LDPC_GDBF_TICKETS) red[64] = (int)nxt;
         }
         __syncthreads();
+        if (LDPC_GDBF_TICKETS) {
+            b = red[64];   // rewritten only after the next codeword's barriers
+            if (tid == 0 && b < a.batch) nxt = gridDim.x + atomicAdd(a.ticket, 1u);
+        } else {
+            b += gridDim.x;
+        }
     }
 }
 
@@ -711,6 +727,11 @@ GdbfChoice gdbf_choose(const DevGraph &g, bool f64, int flags, int maxdv, int ma
 template <typename F, int SRC, int DVM, int NT>
 static hipError_t gdbf_rows_launch_b(const DevGraph &g, const GdbfArgs &a, int num_cus, hipStream_t s)
 {
+    if (LDPC_GDBF_TICKETS) {
+        if (!a.ticket) return hipErrorInvalidValue;
+        const hipError_t e = hipMemsetAsync(a.ticket, 0, sizeof(unsigned), s);
+        if (e != hipSuccess) return e;
+    }
     const GdbfRowsLayout L = gdbf_rows_layout(g.N, g.M, (int)sizeof(F));
     auto fn = k_gdbf_rows<F, SRC, DVM, NT>;
     int per_cu = 0;
