@@ -236,6 +236,23 @@ def test_ems_sim_independent_of_batch_split(nbctx):
 
 
 @pytest.mark.gpu
+def test_ems_ticketed_codewords_independent_of_batch_split():
+    """More codewords than blocks (256): past the first grid they come from the ticket
+    counter in completion order (nb.hip k_ems); the per-frame records must not depend on it."""
+    native = _native()
+    from ldpcsimulation_amd import codes
+    g = native.NbGraph.from_alist(codes.ensure_gf16_code())
+    ctx = native.NbContext(g, 0, 2048)
+    cfg = native.EmsConfig(T=12)
+    full, cf = ctx.sim_batch(2.0, 0.5, cfg, seed=8, stream_id=2, first_cw=0, batch=2048)
+    a, ca = ctx.sim_batch(2.0, 0.5, cfg, seed=8, stream_id=2, first_cw=0, batch=700)
+    b, cb = ctx.sim_batch(2.0, 0.5, cfg, seed=8, stream_id=2, first_cw=700, batch=1348)
+    assert np.array_equal(full, np.concatenate([a, b]))
+    assert cf.frames == 2048 and cf.iters == ca.iters + cb.iters
+    assert len(set(full["iters"].tolist())) > 3
+
+
+@pytest.mark.gpu
 def test_ems_waterfall(nbctx):
     """FER falls with Eb/N0, early-stopped frames are codewords (parity unpinned: no reference FER)."""
     native = _native()

@@ -213,6 +213,22 @@ def test_gdbf_sim_independent_of_batch_split(gpu_ctx_factory):
 
 
 @pytest.mark.gpu
+def test_gdbf_ticketed_codewords_independent_of_batch_split(gpu_ctx_factory):
+    """More codewords than the rows kernel's grid: past the first grid they are handed out
+    by the ticket counter, in whatever order blocks finish -- the per-frame records and
+    counts must not depend on it (gdbf.hip k_gdbf_rows)."""
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory("80211n_1944_r12.alist", 8192)
+    cfg = native.GdbfConfig(T=60)
+    full, cf = ctx.gdbf_sim_batch(3.0, 0.5, cfg, seed=9, stream_id=1, first_cw=0, batch=8192)
+    a, ca = ctx.gdbf_sim_batch(3.0, 0.5, cfg, seed=9, stream_id=1, first_cw=0, batch=3000)
+    b, cb = ctx.gdbf_sim_batch(3.0, 0.5, cfg, seed=9, stream_id=1, first_cw=3000, batch=5192)
+    assert np.array_equal(full, np.concatenate([a, b]))
+    assert cf.frames == 8192 and cf.bit_err == ca.bit_err + cb.bit_err and cf.iters == ca.iters + cb.iters
+    assert len(set(full["iters"].tolist())) > 5   # codewords of unequal length: the tickets matter
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("code", ["80211n_1944_r12.alist", "PEGReg504x1008.alist", "4000.2000.4.244.alist"])
 @pytest.mark.parametrize("vname", ["SMNGDBF", "MNGDBF", "ATGDBF", "SATGDBF", "QSMNGDBF"])
 @pytest.mark.parametrize("prec", ["f64", "f32"])
