@@ -597,9 +597,24 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         se += dv != cs;
         if (a.d_out) a.d_out[(size_t)b * N + v] = (uint8_t)dv;
     }
+    // block sums: wave shuffles, lane 0 adds into the totals red[65..67] (LDS atomics),
+    // one barrier, thread 0 reads and clears them; the caller's ticket barrier ends the
+    // codeword (k_ems)
     int sums[3] = {be, se, unc};
-    block_sum_n<3>(sums, red);
+    int *tot = red + 65;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sums[v] += __shfl_xor(sums[v], o, 64);
+        if ((tid & 63) == 0 && sums[v]) atomicAdd(&tot[v], sums[v]);
+    }
+    __syncthreads();
     if (tid == 0) {
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+            sums[v] = tot[v];
+            tot[v] = 0;
+        }
         atomicAdd(&a.counts[0], (unsigned long long)sums[0]);
         atomicAdd(&a.counts[1], (unsigned long long)(sums[1] > 0));
         atomicAdd(&a.counts[2], (unsigned long long)sums[2]);
@@ -609,7 +624,6 @@ __device__ __forceinline__ void ems_codeword(const NbArgs &a, const NbDevGraph &
         atomicAdd(&a.counts[6], (unsigned long long)sums[1]);
         if (a.frame_res) a.frame_res[b] = make_int4(sums[0], sums[2], fail, it);
     }
-    __syncthreads();
     EMS_LAP(6);
 #ifdef LDPC_EMS_STAMPS
     st.v[7] += 1;
@@ -627,7 +641,7 @@ __host__ __device__ inline size_t aux_bytes(const NbDevGraph &g)
 {
     return align16((size_t)g.N * g.m * 4) + align16((size_t)g.N) + align16((size_t)g.M) +
            align16((size_t)g.N * 4) + align16((size_t)g.E * 2) + align16((size_t)g.E) +
-           align16((size_t)(g.M + 3) / 4 * 4) + (16 * 3 + 16 + 4) * 4;
+           align16((size_t)(g.M + 3) / 4 * 4) + (16 * 3 + 16 + 4 + 4) * 4;
 }
 
 template <int Q, int MB, int DC, int SRC, bool GSTATE, int THREADS>
@@ -658,8 +672,9 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
     p += align16((size_t)g.E);
     uint32_t *synd = reinterpret_cast<uint32_t *>(p);   // check j: byte j & 3 of word j >> 2
     p += align16((size_t)(g.M + 3) / 4 * 4);
-    int *red = reinterpret_cast<int *>(p);   // block_sum_n scratch [0, 48), wave flags [48, 64), the ticket [64]
+    int *red = reinterpret_cast<int *>(p);   // [48, 64) wave flags, [64] the ticket, [65, 68) the block totals
     for (int w = threadIdx.x; w < (g.M + 3) / 4; w += blockDim.x) synd[w] = 0u;
+    if (threadIdx.x < 3) red[65 + threadIdx.x] = 0;   // the block totals (ems_codeword)
     for (int j = threadIdx.x; j < g.M; j += blockDim.x) cn_d[j] = (uint8_t)(g.row_ptr[j + 1] - g.row_ptr[j]);
     for (int v = threadIdx.x; v < g.N; v += blockDim.x)
         vn[v] = ((uint32_t)g.col_ptr[v] << 8) | (uint32_t)(g.col_ptr[v + 1] - g.col_ptr[v]);
@@ -679,9 +694,9 @@ __global__ __launch_bounds__(THREADS) void k_ems(NbArgs a, NbDevGraph g, float *
     if (LDPC_EMS_TICKETS && threadIdx.x == 0) nxt = gridDim.x + atomicAdd(a.ticket, 1u);
     for (int b = blockIdx.x; b < a.batch;) {
         ems_codeword<Q, MB, DC, SRC, GSTATE>(a, g, b, msg, lam, dec, sc, red, synd, st);
+        if (LDPC_EMS_TICKETS && threadIdx.x == 0) red[64] = (int)nxt;
+        __syncthreads();   // the codeword's end (its totals read, the next ticket published)
         if (LDPC_EMS_TICKETS) {
-            if (threadIdx.x == 0) red[64] = (int)nxt;
-            __syncthreads();
             b = red[64];
             if (threadIdx.x == 0 && b < a.batch) nxt = gridDim.x + atomicAdd(a.ticket, 1u);
         } else {
