@@ -110,10 +110,11 @@ variant:
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(VARDIR)/obj_$(NAME)/kernels.o $(VARDIR)/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/nb_graph.o $(LIBDIR)/obj/graph.o
 
-# Fast row kernel A/B variants: make fastvariant NAME=x VFLAGS="-DLDPC_FAST_..." -> ab/libldpc_hip_x.so
+# Fast row kernel A/B variants: make fastvariant NAME=x VFLAGS="-DLDPC_FAST_..." [FASTSRC=file] -> ab/libldpc_hip_x.so
+FASTSRC ?= $(CSRC)/rows_fast.hip
 fastvariant: $(OBJS)
 	mkdir -p $(VARDIR)/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/rows_fast.o $(CSRC)/rows_fast.hip
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/rows_fast.o $(FASTSRC)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/rows_fast.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/rows_fast.o
 

@@ -60,6 +60,13 @@
 
 namespace ldpc {
 
+// Progress-ordered wave priorities in the check phase: s_setprio 3 at the phase start,
+// one lower after each row, 0 for the bit phase -- a wave behind outranks the ones
+// ahead, so the VALU-bound phase does not end on lone waves (config 1, PEG 1008 fp64
+// MS T=10: 25.6-26.0 -> 26.8-27.0 Gbit/s). 0: none.
+#ifndef LDPC_FAST_PRIOBAL
+#define LDPC_FAST_PRIOBAL 1
+#endif
 #ifndef LDPC_FAST_PREFETCH
 #define LDPC_FAST_PREFETCH 1
 #endif
@@ -233,6 +240,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             for (int q = 0; q < (CPT + 1) / 2; ++q) asm volatile("" : "+v"(vdst2[q]));
             // ---- check nodes (with LDPC_FAST_PREFETCH, row r+1's gathers are issued
             // before row r is computed) ----
+            if (LDPC_FAST_PRIOBAL) __builtin_amdgcn_s_setprio(3);
             P xin[LDPC_FAST_PREFETCH ? 2 : 1][DC];
 #pragma unroll
             for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(LDPC_FAST_EXP == 5 ? app_base + 8 * k : addr8<DC>(colw[0], k, app_base));
@@ -257,13 +265,23 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                 } else {
                     ok = cn_fast<DC, C>(xin[r % NB], prev[r], VAR == V_NMS, (float)alpha, (float)rcp);
                 }
-                if (!ok && deg[r] > 0) red[31] = 1;   // rows past M (degree 0) only write dummy slots
+                // a premise break (rows past M, degree 0, only write dummy slots): a skipped
+                // branch, not an exec-masked flag store per row
+                if (__builtin_amdgcn_ballot_w64(!ok && deg[r] > 0)) {
+                    asm volatile(";");   // a side effect: stays a skipped branch
+                    if (!ok && deg[r] > 0) red[31] = 1;
+                }
+                if (LDPC_FAST_PRIOBAL) {
+                    if (r == 0) __builtin_amdgcn_s_setprio(2);
+                    else __builtin_amdgcn_s_setprio(1);
+                }
                 if constexpr (LDPC_FAST_EXP != 1) {
 #pragma unroll
                     for (int k = 0; k < DC; ++k) lds_put<P>(addr8<DC>(posw[r], k, c2v_base), prev[r][k]);
                 }
                 if (RPT > 1) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
             }
+            if (LDPC_FAST_PRIOBAL) __builtin_amdgcn_s_setprio(0);
             if constexpr (LDPC_FAST_EXP != 3) __syncthreads();
             flag = red[31];   // in flight during the bit phase
             // ---- bit nodes: sum = yq + c2v in nlist order (:452-476) ----
