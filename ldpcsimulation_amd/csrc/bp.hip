@@ -217,6 +217,13 @@ static bool bp_rows_fits(const DevGraph &g, int E, bool f64)
     return L.total <= 150 * 1024 && (size_t)g.M * 8 * 2 <= (size_t)(L.total - L.msg_off);   // + the prologue's slot map
 }
 
+// Progress-ordered wave priorities in the rows kernel's check phase: s_setprio 3 at the
+// phase start, 2 after the first row, 0 for the bit phase (a wave behind outranks the
+// ones ahead: the transcendental-heavy phase does not end on lone waves; N=1944 T=50:
+// fp32 47.1 -> 41.3 ms, fp64 53.8 -> 51.2 ms). 0: none.
+#ifndef LDPC_BP_PRIOBAL
+#define LDPC_BP_PRIOBAL 1
+#endif
 #ifndef LDPC_BP_ROWS_WAVES
 #define LDPC_BP_ROWS_WAVES 8   // 512-thread fp32 instance: 64 VGPRs, 4 workgroups per CU (11.9 vs 14.2 ms at 4)
 #endif
@@ -335,8 +342,10 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
 #pragma unroll
                 for (int k = 0; k < DC / 2; ++k) asm volatile("" : "+v"(rc[r][k]), "+v"(rp[r][k]));
             // ---- check nodes (:353-377) ----
+            if (LDPC_BP_PRIOBAL) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
             for (int r = 0; r < RPT; ++r) {
+                if (LDPC_BP_PRIOBAL && r > 0) __builtin_amdgcn_s_setprio(2);
                 F th[DC];
 #pragma unroll
                 for (int k = 0; k < DC; ++k) {
@@ -362,6 +371,7 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
                     if (jj < rdeg[r]) msg[(rp[r][jj / 2] >> (16 * (jj & 1))) & 0xffffu] = o;
                 }
             }
+            if (LDPC_BP_PRIOBAL) __builtin_amdgcn_s_setprio(0);
             __syncthreads();
             // ---- bit nodes: sum in nlist order (:384-393) ----
             if (own) {
