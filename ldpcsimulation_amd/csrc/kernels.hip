@@ -577,6 +577,12 @@ __global__ __launch_bounds__(256) void k_flood_init(DecodeArgs a, DevGraph g, Fl
     if ((threadIdx.x & 63) == 0 && unc) atomicAdd(&unc_out[r], unc);
 }
 
+// Progress-ordered wave priorities in k_decode_rows' check phase: s_setprio 3 at the
+// phase start, 2 after the first row, 0 for the bit phase (fp32 OMS on N=1944, T=50:
+// 13.2 -> 11.6 ms; PEG 1008 fp32 MS T=10 +3 %). 0: none.
+#ifndef LDPC_ROWS_PRIOBAL
+#define LDPC_ROWS_PRIOBAL 1
+#endif
 #ifndef LDPC_FLOOD_CPW
 #define LDPC_FLOOD_CPW 8
 #endif
@@ -1647,10 +1653,12 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
                 // ---- check nodes (:410-450, :494-515); row r+1's gathers are issued
                 // before row r is computed ----
                 P xin[2][DC];
+                if (LDPC_ROWS_PRIOBAL) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
                 for (int k = 0; k < DC; ++k) xin[0][k] = app[u16_at<DC>(colw[0], k)];   // padding edges read +INF
 #pragma unroll
                 for (int r = 0; r < RPT; ++r) {
+                    if (LDPC_ROWS_PRIOBAL && r > 0) __builtin_amdgcn_s_setprio(2);
                     if (r + 1 < RPT) {
 #pragma unroll
                         for (int k = 0; k < DC; ++k) xin[(r + 1) & 1][k] = app[u16_at<DC>(colw[r + 1 < RPT ? r + 1 : r], k)];
@@ -1675,6 +1683,7 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
                     if (RPT > 1) __builtin_amdgcn_sched_barrier(0);
 #endif
                 }
+                if (LDPC_ROWS_PRIOBAL) __builtin_amdgcn_s_setprio(0);
                 __syncthreads();
                 if (FAST) flag = red[31];
                 STAMP(t_vn0);
