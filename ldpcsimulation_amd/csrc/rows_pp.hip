@@ -64,6 +64,16 @@ namespace {
 #endif
 // Timing ablations of the per-step work (results wrong by design): 1 no channel
 // generation, 2 no syndrome / decisions, 4 no block reduction.
+// Bit mask of the precisions (1 fp32 pairs, 2 fp64) whose step tail is folded into the
+// last intervals: the bit role takes a slot's decisions and error weights from the sums of
+// that slot's last bit-node pass (the values it writes to app), and the check role forms
+// slot 0's syndrome in the extra interval, where it is idle; only slot 1's syndrome stays
+// after the last barrier. Otherwise all of it follows the last barrier. Measured: fp32
+// 7.16-7.21 -> 7.10-7.12 ms; fp64 12.28-12.29 -> 12.31 (the decisions lengthen the
+// check-bound interval of bit(0,T-1)), so fp64 keeps the tail after the barrier.
+#ifndef LDPC_PP_TAILFUSE
+#define LDPC_PP_TAILFUSE 1
+#endif
 #ifndef LDPC_PP_TAILEXP
 #define LDPC_PP_TAILEXP 0
 #endif
@@ -398,9 +408,12 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
     PP_STAMP_DECL;
     for (int grp = blockIdx.x; grp < nsteps; grp += gridDim.x) {
         [[maybe_unused]] uint32_t pacc[2] = {0u, 0u};   // fp64, LDPC_PP_STICKY: per-slot premise maximum
+        constexpr bool TF = (LDPC_PP_TAILFUSE & (F64 ? 2 : 1)) != 0;
         int unc[2 * C];
+        [[maybe_unused]] int wdec[2 * C];   // LDPC_PP_TAILFUSE: bit errors per codeword (bit role)
+        [[maybe_unused]] int synd0[C];      // LDPC_PP_TAILFUSE: slot 0's syndrome (check role)
 #pragma unroll
-        for (int q = 0; q < 2 * C; ++q) unc[q] = 0;
+        for (int q = 0; q < 2 * C; ++q) unc[q] = wdec[q] = 0;
         if constexpr (HB) {
             if (!(LDPC_PP_TAILEXP & 1)) {
                 pp_channel<F, SRC>(a, s, N, grp, unc, bt, kPPRole);
@@ -451,9 +464,49 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
         }
         __syncthreads();   // B2: yq in app
 
+        // Decisions and error weight of slot Y's codewords from its final posteriors
+        // (bit slots; :270, :382-393), into w[Y*C + c].
+        auto decide = [&](int Y, const P *post, int *w) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int q = Y * C + c, b = grp * 2 * C + q;
+                if (b >= a.batch) continue;
+                const int8_t *cvec =
+                    SRC == SRC_GIVEN ? (a.c ? a.c + (size_t)b * N : nullptr)
+                                     : (a.cw_table ? a.cw_table + (size_t)((a.first_cw + (uint64_t)b) % (uint64_t)a.cw_rows) * N
+                                                   : nullptr);
+                int e = 0;
+#pragma unroll
+                for (int i = 0; i < CPT; ++i) {
+                    const int v = vdst(i);
+                    if (v < N) {
+                        const int d = post[i].v[c] > F(0) ? 1 : -1;   // :471-474
+                        const int cv = cvec ? cvec[v] : 1;
+                        e += (d != cv);
+                        if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
+                    }
+                }
+                w[q] = e;
+            }
+        };
+        // Syndrome of slot X's codeword c (rows; padding edges read +inf: parity 0; rows past M skipped)
+        auto syndrome = [&](int X, int c) -> int {
+            int synd = 0;
+            if constexpr (R > 0) {
+                static_for<0, R>([&](auto rc) {
+                    constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
+                    int par = 0;
+#pragma unroll
+                    for (int k = 0; k < DCr; ++k) par ^= (s.app[X][u16_at<DCX>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
+                    synd |= deg[r] > 0 ? par : 0;
+                });
+            }
+            return synd;
+        };
+
         // One barrier interval: the rows of slot X (their reads first), the bit
         // nodes of slot 1 - X when `bits` (HB waves), then the rows' check nodes.
-        auto interval = [&](auto Xc, bool rows, bool bits) {
+        auto interval = [&](auto Xc, bool rows, bool bits, bool last) {
             constexpr int X = decltype(Xc)::value, Y = 1 - X;
             [[maybe_unused]] P xin[RR][DCX];
             if constexpr (R > 0) {
@@ -491,6 +544,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                     vn_phases<F, C, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum);
 #pragma unroll
                     for (int i = 0; i < CPT; ++i) s.app[Y][vdst(i)] = sum[i];
+                    if (TF && last) decide(Y, sum, wdec);   // slot Y's final pass
                 }
             }
             if constexpr (R > 0) {
@@ -537,14 +591,18 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
             }
         };
         for (int it = 0; it < a.T; ++it) {
-            interval(std::integral_constant<int, 0>(), true, it > 0);
+            interval(std::integral_constant<int, 0>(), true, it > 0, false);
             PP_BARRIER();   // | check(0,it) | bit(1,it-1) |
-            interval(std::integral_constant<int, 1>(), true, true);
+            interval(std::integral_constant<int, 1>(), true, true, it == a.T - 1);
             PP_BARRIER();   // | check(1,it) | bit(0,it) |
         }
         if (a.T > 0) {
-            interval(std::integral_constant<int, 0>(), false, true);
-            PP_BARRIER();   // | -- | bit(1,T-1) |
+            interval(std::integral_constant<int, 0>(), false, true, true);
+            if (TF && !(LDPC_PP_TAILEXP & 2)) {   // slot 0's posteriors are final
+#pragma unroll
+                for (int c = 0; c < C; ++c) synd0[c] = syndrome(0, c);
+            }
+            PP_BARRIER();   // | syndrome(0) | bit(1,T-1) |
         }
         if constexpr (F64 && R > 0 && LDPC_PP_STICKY) {   // the premise of every iteration of the step
             if (pacc[0] >= kFast64MaxHi && LDPC_PP_EXP == 0) s.red[0] = 1;
@@ -556,49 +614,29 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
             pp_account<C, HB>(a, s.red, grp, sums, redo, acc);
             continue;
         }
-        // syndrome (rows; padding edges read +inf: parity 0; rows past M skipped) and
-        // decisions / error weight (bit slots; :270, :382-393) of the step's codewords
+        // syndrome and decisions / error weight of the step's codewords (what the last
+        // intervals have not formed already, LDPC_PP_TAILFUSE; T = 0: all of it here)
+        const bool fused = TF && a.T > 0;
+        if constexpr (HB) {
+            if (!fused) {
+#pragma unroll
+                for (int X = 0; X < 2; ++X) {
+                    P post[CPT];
+#pragma unroll
+                    for (int i = 0; i < CPT; ++i) post[i] = s.app[X][vdst(i) <= N ? vdst(i) : 0];
+                    decide(X, post, wdec);
+                }
+            }
+        }
         int sums[6 * C];
 #pragma unroll
         for (int X = 0; X < 2; ++X) {
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 const int q = X * C + c;
-                sums[3 * q] = 0;
+                sums[3 * q] = wdec[q];
                 sums[3 * q + 1] = unc[q];
-                sums[3 * q + 2] = 0;
-                if constexpr (R > 0) {
-                    int synd = 0;
-                    static_for<0, R>([&](auto rc) {
-                        constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
-                        int par = 0;
-#pragma unroll
-                        for (int k = 0; k < DCr; ++k) par ^= (s.app[X][u16_at<DCX>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
-                        synd |= deg[r] > 0 ? par : 0;
-                    });
-                    sums[3 * q + 2] = synd;
-                }
-                if constexpr (HB) {
-                    const int b = grp * 2 * C + q;
-                    if (b < a.batch) {
-                        const int8_t *cvec =
-                            SRC == SRC_GIVEN ? (a.c ? a.c + (size_t)b * N : nullptr)
-                                             : (a.cw_table ? a.cw_table + (size_t)((a.first_cw + (uint64_t)b) % (uint64_t)a.cw_rows) * N
-                                                           : nullptr);
-                        int w = 0;
-#pragma unroll
-                        for (int i = 0; i < CPT; ++i) {
-                            const int v = vdst(i);
-                            if (v < N) {
-                                const int d = s.app[X][v].v[c] > F(0) ? 1 : -1;   // :471-474
-                                const int cv = cvec ? cvec[v] : 1;
-                                w += (d != cv);
-                                if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
-                            }
-                        }
-                        sums[3 * q] = w;
-                    }
-                }
+                sums[3 * q + 2] = (X == 0 && fused) ? synd0[c] : syndrome(X, c);
             }
         }
         pp_account<C, HB>(a, s.red, grp, sums, redo, acc);
