@@ -101,4 +101,28 @@ __device__ __forceinline__ void block_sum_n(int (&x)[NV], int *red)
     }
 }
 
+// Block sums with one barrier: wave sums by shuffles, one ds_add per wave and value into
+// the LDS totals tot[0..NV) (zero on entry), then thread 0 reads the totals into x and
+// zeroes them. The caller orders that zeroing before its next use (a later barrier).
+template <int NV>
+__device__ __forceinline__ void block_sum_lds(int (&x)[NV], int *tot)
+{
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x[v] += __shfl_xor(x[v], o, 64);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (x[v]) atomicAdd(&tot[v], x[v]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            x[v] = tot[v];
+            tot[v] = 0;
+        }
+    }
+}
+
 }  // namespace ldpc

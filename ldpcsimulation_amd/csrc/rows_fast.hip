@@ -140,9 +140,12 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
     // overwritten by waves 10-12 of a 1024-thread fp32 pair block)
     static_assert(32 + 16 * 3 * C <= 128, "block sums overlap the accumulators");
     unsigned long long *acc = reinterpret_cast<unsigned long long *>(red + 128);
-    if (tid == 0)
+    if (tid == 0) {
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
+#pragma unroll
+        for (int q = 0; q < 3 * C; ++q) red[32 + q] = 0;   // block_sum_lds totals
+    }
     for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
         // ---- channel (:214-238), staged through the c2v area ----
         if (tid == 0) red[31] = 0;
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                 const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
                 for (int g4 = tid; g4 * 4 < N; g4 += nt) {
                     uint32_t u[4];
-                    philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                    philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
                     F n[4];
                     box_muller(u[0], u[1], n[0], n[1]);
                     box_muller(u[2], u[3], n[2], n[3]);
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             sums[3 * c + 1] = unc[c];
             sums[3 * c + 2] = synd;
         }
-        block_sum_n<3 * C>(sums, red + 32);
+        block_sum_lds<3 * C>(sums, red + 32);   // re-zeroed by thread 0; the step's last barrier orders it
         if (tid == 0) {
 #pragma unroll
             for (int c = 0; c < C; ++c) {
