@@ -280,6 +280,8 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
     if (tid == 0) {
         app[N] = F(0);
         msg[E] = -F(0);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) red[q] = 0;   // block_sum_lds totals
     }
     const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
 
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
                 for (int q = 0; q < 4; ++q) yv[q] = (v0 + q < N) ? y[v0 + q] : F(1);
             } else {
                 uint32_t u[4];
-                philox4x32_10((uint32_t)tid, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                philox4x32_10<true>((uint32_t)tid, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
                 F n[4];
                 box_muller(u[0], u[1], n[0], n[1]);
                 box_muller(u[2], u[3], n[2], n[3]);
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
             synd |= par;
         }
         int sums[3] = {w, unc, synd};
-        block_sum_n<3>(sums, red);
+        block_sum_lds<3>(sums, red);   // re-zeroed by thread 0; the step's last barrier orders it
         if (tid == 0) {
             const int sf = sums[2] > 0;
             atomicAdd(&a.counts[0], (unsigned long long)sums[0]);

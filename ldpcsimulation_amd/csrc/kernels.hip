@@ -580,6 +580,17 @@ __global__ __launch_bounds__(256) void k_flood_init(DecodeArgs a, DevGraph g, Fl
 // Progress-ordered wave priorities in k_decode_rows' check phase: s_setprio 3 at the
 // phase start, 2 after the first row, 0 for the bit phase (fp32 OMS on N=1944, T=50:
 // 13.2 -> 11.6 ms; PEG 1008 fp32 MS T=10 +3 %). 0: none.
+// A/B switches of the row kernel's per-step work: block sums with one barrier into LDS
+// totals (block_sum_lds, 1) vs block_sum_n (0); Philox products by v_mad_u64_u32.
+// Measured (fp32, 65 536 codewords): block_sum_lds makes PEG 1008 MS T=10 39.6 -> 42.3
+// Gbit/s but N=1944 OMS T=50 11.0 -> 10.1 (the same instance; a code-layout effect, not
+// the reduction's own cost), so the default stays 0; v_mad_u64_u32 is neutral and kept.
+#ifndef LDPC_ROWS_ACCT
+#define LDPC_ROWS_ACCT 0
+#endif
+#ifndef LDPC_ROWS_MAD64
+#define LDPC_ROWS_MAD64 1
+#endif
 #ifndef LDPC_ROWS_PRIOBAL
 #define LDPC_ROWS_PRIOBAL 1
 #endif
@@ -1518,6 +1529,8 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
 #pragma unroll
         for (int c = 0; c < C; ++c) inf.v[c] = dinf<F>();
         app[N] = inf;
+#pragma unroll
+        for (int q = 0; q < 3 * C; ++q) red[32 + q] = 0;   // block_sum_lds totals
     }
 
     // The second-dispatched half of the workgroup at priority 1 for the whole
@@ -1558,7 +1571,7 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
                 const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
                 for (int g4 = tid; g4 * 4 < N; g4 += nt) {
                     uint32_t u[4];
-                    philox4x32_10((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                    philox4x32_10<LDPC_ROWS_MAD64 != 0>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
                     F n[4];
                     box_muller(u[0], u[1], n[0], n[1]);
                     box_muller(u[2], u[3], n[2], n[3]);
@@ -1744,7 +1757,8 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
             sums[3 * c + 1] = unc[c];
             sums[3 * c + 2] = synd;
         }
-        block_sum_n<3 * C>(sums, red + 32);
+        if (LDPC_ROWS_ACCT) block_sum_lds<3 * C>(sums, red + 32);   // re-zeroed by thread 0; the step's last barrier orders it
+        else block_sum_n<3 * C>(sums, red + 32);
         if (tid == 0) {
 #pragma unroll
             for (int c = 0; c < C; ++c) {
