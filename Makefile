@@ -17,6 +17,16 @@ CLIS      = $(BINDIR)/decodeMinSum $(BINDIR)/decodeNMS $(BINDIR)/decodeNormalize
             $(BINDIR)/decodeMNGDBF $(BINDIR)/decodeSMNGDBF $(BINDIR)/decodeATGDBF $(BINDIR)/decodeSATGDBF $(BINDIR)/decodeSMGDBF $(BINDIR)/decodeBP \
             $(BINDIR)/decodeSGDBF $(BINDIR)/decodeMGDBF $(BINDIR)/decodeStochasticNGDBF
 
+# VFLAGS (-D switches of the A/B experiments, some of them wrong-result by design) belong
+# to the *variant targets, which build into ab/ with -DLDPC_AB_BUILD; the product refuses
+# them here, and the kernel sources refuse the wrong-result ones without LDPC_AB_BUILD.
+PRODUCT_GOALS = all $(LIB) $(OBJS) $(CLIS)
+ifneq ($(strip $(VFLAGS)),)
+ifneq ($(filter $(PRODUCT_GOALS),$(if $(MAKECMDGOALS),$(MAKECMDGOALS),all)),)
+$(error VFLAGS="$(VFLAGS)" is for the A/B targets (make ppvariant/fastvariant/nbvariant/...), not the product)
+endif
+endif
+
 all: $(LIB) $(CLIS) oracle
 
 $(LIBDIR)/obj:
@@ -105,8 +115,8 @@ $(BINDIR)/decodeStochasticNGDBF: $(GDBF_SRC) $(LIB) $(CSRC)/cli_common.h | $(BIN
 # Kernel A/B variants: make variant NAME=x VFLAGS="-DLDPC_..." -> ab/libldpc_hip_x.so
 variant:
 	mkdir -p $(VARDIR)/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(NOSLP) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/api.o $(CSRC)/api.cpp
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(NOSLP) -DLDPC_AB_BUILD $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/kernels.o $(CSRC)/kernels.hip
+	$(HIPCC) $(HIPFLAGS) -DLDPC_AB_BUILD $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/api.o $(CSRC)/api.cpp
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(VARDIR)/obj_$(NAME)/kernels.o $(VARDIR)/obj_$(NAME)/api.o $(LIBDIR)/obj/rows_fast.o $(LIBDIR)/obj/rows_pp.o $(LIBDIR)/obj/gdbf.o $(LIBDIR)/obj/bp.o $(LIBDIR)/obj/nb.o $(LIBDIR)/obj/nb_api.o $(LIBDIR)/obj/nb_graph.o $(LIBDIR)/obj/graph.o
 
@@ -114,14 +124,14 @@ variant:
 FASTSRC ?= $(CSRC)/rows_fast.hip
 fastvariant: $(OBJS)
 	mkdir -p $(VARDIR)/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/rows_fast.o $(FASTSRC)
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) -DLDPC_AB_BUILD $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/rows_fast.o $(FASTSRC)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/rows_fast.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/rows_fast.o
 
 # Ping-pong kernel A/B variants: make ppvariant NAME=x VFLAGS="-DLDPC_PP_..." -> ab/libldpc_hip_x.so
 ppvariant: $(OBJS)
 	mkdir -p $(VARDIR)/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/rows_pp.o $(PPSRC)
+	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) -DLDPC_AB_BUILD $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/rows_pp.o $(PPSRC)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/rows_pp.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/rows_pp.o
 
@@ -135,21 +145,21 @@ clean-ab:
 NBSRC ?= $(CSRC)/nb.hip
 nbvariant: $(OBJS)
 	mkdir -p $(VARDIR)/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(NOSLP) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/nb.o $(NBSRC)
+	$(HIPCC) $(HIPFLAGS) $(NOSLP) -DLDPC_AB_BUILD $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/nb.o $(NBSRC)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/nb.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/nb.o
 
 # GDBF kernel A/B variants: make gdbfvariant NAME=x VFLAGS="-DLDPC_GDBF_..." -> ab/libldpc_hip_x.so
 gdbfvariant: $(OBJS)
 	mkdir -p $(VARDIR)/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(NOSLP) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/gdbf.o $(CSRC)/gdbf.hip
+	$(HIPCC) $(HIPFLAGS) $(NOSLP) -DLDPC_AB_BUILD $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/gdbf.o $(CSRC)/gdbf.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/gdbf.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/gdbf.o
 
 # BP kernel A/B variants: make bpvariant NAME=x VFLAGS="-DLDPC_BP_..." -> ab/libldpc_hip_x.so
 bpvariant: $(OBJS)
 	mkdir -p $(VARDIR)/obj_$(NAME)
-	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/bp.o $(CSRC)/bp.hip
+	$(HIPCC) $(HIPFLAGS) -DLDPC_AB_BUILD $(VFLAGS) -c -o $(VARDIR)/obj_$(NAME)/bp.o $(CSRC)/bp.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/bp.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/bp.o
 

@@ -155,7 +155,10 @@ int  ldpc_device_count(int *n);
  * max_batch bounds the frames of one decode/sim call. */
 int  ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **out);
 /* Launch on an external hipStream_t (e.g. torch.cuda.current_stream()); NULL
- * restores the context's own stream. */
+ * restores the context's own stream. A context's launches share its counters and
+ * buffers, so a stream change is ordered after the work already queued on the
+ * previous stream (an event): one context's launches never overlap. Use one
+ * context per stream for concurrent launches. */
 int  ldpc_ctx_set_stream(ldpc_ctx *ctx, void *hip_stream);
 int  ldpc_ctx_synchronize(ldpc_ctx *ctx);
 void ldpc_ctx_destroy(ldpc_ctx *ctx);
@@ -261,7 +264,8 @@ typedef enum {
     LDPC_OPT_EMS_SWIZZLE = 21      /* EMS (nb context): 0 swizzled message slots, 1 the plain layout          */
 } ldpc_option;
 #define LDPC_OPT_COUNT 22
-/* LDPC_ERR_INVALID for an unknown option or a value outside its range. */
+/* LDPC_ERR_INVALID for an unknown option, a value outside its range, or an
+ * EMS option (LDPC_OPT_EMS_*: the nb context's, ldpc_nb_ctx_set_option). */
 int  ldpc_ctx_set_option(ldpc_ctx *ctx, int option, int value);
 int  ldpc_ctx_get_option(const ldpc_ctx *ctx, int option, int *value);
 

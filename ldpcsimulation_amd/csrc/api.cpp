@@ -78,6 +78,7 @@ struct ldpc_ctx {
     DevBuf graph, counts, hist, y_stage, c_stage, d_stage, fw_stage, cw_table, gscratch, p_stage;
     int cw_rows = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t handoff = nullptr;  // orders the launches of a context across ldpc_ctx_set_stream
     ldpc::AuxStream aux;          // second stream of the flooding phase launches (kernels.h)
     bool timed = false;
     ldpc::Options opts;           // kernel-selection options (ldpc_ctx_set_option), tests and A/B only
@@ -284,6 +285,7 @@ static void ctx_free(ldpc_ctx *c)
         b->release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->handoff) (void)hipEventDestroy(c->handoff);
     if (c->aux.fork) (void)hipEventDestroy(c->aux.fork);
     if (c->aux.join) (void)hipEventDestroy(c->aux.join);
     if (c->aux.s) (void)hipStreamDestroy(c->aux.s);
@@ -457,7 +459,17 @@ int ldpc_ctx_create(int device, const ldpc_graph *g, int max_batch, ldpc_ctx **o
 int ldpc_ctx_set_stream(ldpc_ctx *c, void *s)
 {
     if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
-    c->stream = s ? (hipStream_t)s : c->own;
+    const hipStream_t ns = s ? (hipStream_t)s : c->own;
+    if (ns != c->stream) {
+        // The launches of one context share its counters (the GDBF/EMS codeword ticket
+        // included), staging and re-decode buffers: the new stream starts after everything
+        // already queued on the old one, so launches never overlap across a stream change.
+        HIP_TRY(hipSetDevice(c->device));
+        if (!c->handoff) HIP_TRY(hipEventCreateWithFlags(&c->handoff, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->handoff, c->stream));
+        HIP_TRY(hipStreamWaitEvent(ns, c->handoff, 0));
+    }
+    c->stream = ns;
     return LDPC_OK;
 }
 
@@ -476,6 +488,8 @@ int ldpc_ctx_set_option(ldpc_ctx *c, int option, int value)
     if (!c) return set_err(LDPC_ERR_INVALID, "ctx is null");
     if (!ldpc::option_value_ok(option, value))
         return set_err(LDPC_ERR_INVALID, "option %d: unknown, or value %d out of range", option, value);
+    if (ldpc::option_is_ems(option))
+        return set_err(LDPC_ERR_INVALID, "option %d is an EMS option (ldpc_nb_ctx_set_option)", option);
     c->opts.v[option] = value;
     return LDPC_OK;
 }

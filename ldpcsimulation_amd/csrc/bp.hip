@@ -143,7 +143,7 @@ __device__ __forceinline__ void bp_codeword(const DecodeArgs &a, const DevGraph 
         synd |= par;
     }
     int sums[3] = {w, unc, synd};
-    block_sum_n<3>(sums, red);
+    block_sum_n_t0<3>(sums, red);
     if (tid == 0) {
         const int sf = sums[2] > 0;
         atomicAdd(&a.counts[0], (unsigned long long)sums[0]);

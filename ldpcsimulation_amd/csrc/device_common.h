@@ -56,6 +56,9 @@ __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, float &n0, 
 #ifndef LDPC_BM64
 #define LDPC_BM64 0
 #endif
+#if LDPC_BM64 != 0 && !defined(LDPC_AB_BUILD)
+#error "LDPC_BM64 changes the noise the parity tests pin: variant builds only"
+#endif
 __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, double &n0, double &n1)
 {
     if constexpr (!LDPC_BM64) {
@@ -77,7 +80,7 @@ __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, double &n0,
 // Sums of NV values over the workgroup with one barrier pair; red holds 16*NV ints.
 // The totals are valid in thread 0 only.
 template <int NV>
-__device__ __forceinline__ void block_sum_n(int (&x)[NV], int *red)
+__device__ __forceinline__ void block_sum_n_t0(int (&x)[NV], int *red)
 {
 #pragma unroll
     for (int v = 0; v < NV; ++v)

@@ -300,7 +300,7 @@ __device__ __forceinline__ void gdbf_codeword(const GdbfArgs &a, const DevGraph 
         synd |= p;
     }
     int sums[3] = {wgt, unc, synd};
-    block_sum_n<3>(sums, red);
+    block_sum_n_t0<3>(sums, red);
     if (tid == 0) {
         const int sf = sums[2] > 0;
         atomicAdd(&a.counts[0], (unsigned long long)sums[0]);
@@ -669,7 +669,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
             synd |= (int)p;
         }
         int sums[3] = {wgt, unc, synd};
-        block_sum_n<3>(sums, red);
+        block_sum_n_t0<3>(sums, red);
         if (tid == 0) {
             const int sf = sums[2] > 0;
             atomicAdd(&a.counts[0], (unsigned long long)sums[0]);

@@ -170,14 +170,12 @@ __device__ __forceinline__ void decode_codeword(const DecodeArgs &a, const DevGr
         for (int k = 0; k < deg; ++k) par ^= (app[rc[k]] > F(0)) ? 0 : 1;
         synd |= par;
     }
-    {
-        int sums[3] = {w, unc, synd};
-        block_sum_n<3>(sums, red);
+    int sums[3] = {w, unc, synd};
+    block_sum_n_t0<3>(sums, red);
+    if (tid == 0) {   // the block totals exist in thread 0 only
         w = sums[0];
         unc = sums[1];
         synd = sums[2];
-    }
-    if (tid == 0) {
         atomicAdd(&a.counts[0], (unsigned long long)w);
         atomicAdd(&a.counts[1], (unsigned long long)(w > 0));
         atomicAdd(&a.counts[2], (unsigned long long)unc);
@@ -450,7 +448,7 @@ __global__ __launch_bounds__(512, (sizeof(F) == 4 && DC <= 8) ? 8 : 4) void k_de
             synd |= par;
         }
         int sums[3] = {w, unc, synd};
-        block_sum_n<3>(sums, red + 32);
+        block_sum_n_t0<3>(sums, red + 32);
         if (tid == 0) {
             const int sf = sums[2] > 0;
             acc[0] += (unsigned long long)sums[0];
@@ -581,7 +579,7 @@ __global__ __launch_bounds__(256) void k_flood_init(DecodeArgs a, DevGraph g, Fl
 // phase start, 2 after the first row, 0 for the bit phase (fp32 OMS on N=1944, T=50:
 // 13.2 -> 11.6 ms; PEG 1008 fp32 MS T=10 +3 %). 0: none.
 // A/B switches of the row kernel's per-step work: block sums with one barrier into LDS
-// totals (block_sum_lds, 1) vs block_sum_n (0); Philox products by v_mad_u64_u32.
+// totals (block_sum_lds, 1) vs block_sum_n_t0 (0); Philox products by v_mad_u64_u32.
 // Measured (fp32, 65 536 codewords): block_sum_lds makes PEG 1008 MS T=10 39.6 -> 42.3
 // Gbit/s but N=1944 OMS T=50 11.0 -> 10.1 (the same instance; a code-layout effect, not
 // the reduction's own cost), so the default stays 0; v_mad_u64_u32 is neutral and kept.
@@ -1327,7 +1325,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
         synd |= par;
     }
     int sums[3] = {w, unc, synd};
-    block_sum_n<3>(sums, red);
+    block_sum_n_t0<3>(sums, red);
     if (tid == 0) {
         const int sf = sums[2] > 0;
         acc[0] += (unsigned long long)sums[0];
@@ -1758,7 +1756,7 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
             sums[3 * c + 2] = synd;
         }
         if (LDPC_ROWS_ACCT) block_sum_lds<3 * C>(sums, red + 32);   // re-zeroed by thread 0; the step's last barrier orders it
-        else block_sum_n<3 * C>(sums, red + 32);
+        else block_sum_n_t0<3 * C>(sums, red + 32);
         if (tid == 0) {
 #pragma unroll
             for (int c = 0; c < C; ++c) {

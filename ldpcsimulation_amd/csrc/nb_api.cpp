@@ -84,6 +84,7 @@ struct ldpc_nb_ctx {
     ldpc::NbDevGraph dg{};
     Buf graph, counts, y_stage, c_stage, d_stage, fr_stage, scratch;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t handoff = nullptr;         // orders the launches of a context across ldpc_nb_ctx_set_stream
     bool timed = false;
     const uint8_t *col_h_swz = nullptr;   // device: col_h with the slot swizzles (nb_swizzled_coefficients)
     ldpc::Options opts;                   // kernel-selection options (ldpc_nb_ctx_set_option)
@@ -226,7 +227,16 @@ int ldpc_nb_ctx_create(int device, const ldpc_nb_graph *g, int max_batch, ldpc_n
 int ldpc_nb_ctx_set_stream(ldpc_nb_ctx *c, void *hip_stream)
 {
     if (!c) return err(LDPC_ERR_INVALID, "ctx is null");
-    c->stream = hip_stream ? (hipStream_t)hip_stream : c->own;
+    const hipStream_t ns = hip_stream ? (hipStream_t)hip_stream : c->own;
+    if (ns != c->stream) {
+        // one context's launches share its counters and codeword ticket: the new stream
+        // starts after everything already queued on the old one (no overlap across streams)
+        NB_HIP_TRY(hipSetDevice(c->device));
+        if (!c->handoff) NB_HIP_TRY(hipEventCreateWithFlags(&c->handoff, hipEventDisableTiming));
+        NB_HIP_TRY(hipEventRecord(c->handoff, c->stream));
+        NB_HIP_TRY(hipStreamWaitEvent(ns, c->handoff, 0));
+    }
+    c->stream = ns;
     return LDPC_OK;
 }
 
@@ -237,6 +247,7 @@ void ldpc_nb_ctx_destroy(ldpc_nb_ctx *c)
     (void)hipStreamSynchronize(c->own);
     for (Buf *b : {&c->graph, &c->counts, &c->y_stage, &c->c_stage, &c->d_stage, &c->fr_stage, &c->scratch})
         b->release();
+    if (c->handoff) (void)hipEventDestroy(c->handoff);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -480,7 +491,7 @@ int ldpc_ems_kernel_info(ldpc_nb_ctx *c, char *name, int name_len, int *lds_byte
 int ldpc_nb_ctx_set_option(ldpc_nb_ctx *c, int option, int value)
 {
     if (!c) return err(LDPC_ERR_INVALID, "ctx is null");
-    if (option != LDPC_OPT_EMS_THREADS && option != LDPC_OPT_EMS_SWIZZLE)
+    if (!ldpc::option_is_ems(option))
         return err(LDPC_ERR_INVALID, "option %d is not an EMS option", option);
     if (!ldpc::option_value_ok(option, value)) return err(LDPC_ERR_INVALID, "option %d: value %d out of range", option, value);
     c->opts.v[option] = value;

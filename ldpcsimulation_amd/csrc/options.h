@@ -19,6 +19,10 @@ struct Options {
 // Valid range of each option's value (ldpc_ctx_set_option refuses others).
 bool option_value_ok(int option, int value);
 
+// The EMS options belong to the GF(q) context (ldpc_nb_ctx_set_option) and only there;
+// the binary context refuses them, and the nb context refuses every other option.
+inline bool option_is_ems(int option) { return option == LDPC_OPT_EMS_THREADS || option == LDPC_OPT_EMS_SWIZZLE; }
+
 // The options installed on this thread (all zero when none is).
 const Options &cur_opts();
 inline int opt(int option) { return cur_opts().v[option]; }

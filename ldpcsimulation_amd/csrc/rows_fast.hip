@@ -76,6 +76,11 @@ namespace ldpc {
 #ifndef LDPC_FAST_EXP
 #define LDPC_FAST_EXP 0
 #endif
+// Wrong-result timing switches build only into A/B libraries (the *variant targets define
+// LDPC_AB_BUILD); a product build with one of them set is refused.
+#if LDPC_FAST_EXP != 0 && !defined(LDPC_AB_BUILD)
+#error "LDPC_FAST_EXP != 0 gives wrong results by design: make fastvariant only"
+#endif
 template <int RPT> struct FastShape;
 #ifndef LDPC_FAST_RPT1_WAVES
 #define LDPC_FAST_RPT1_WAVES 4
@@ -136,7 +141,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
     const int ngrp = (a.batch + C - 1) / C;
     // the block's totals (thread 0), added to a.counts once at the end; in the
     // dynamic area (no static LDS: app starts at LDS address 0)
-    // past block_sum_n's area at every block size (16 waves x 3C sums; ADVICE r2: red + 96 was
+    // past block_sum_n_t0's area at every block size (16 waves x 3C sums; ADVICE r2: red + 96 was
     // overwritten by waves 10-12 of a 1024-thread fp32 pair block)
     static_assert(32 + 16 * 3 * C <= 128, "block sums overlap the accumulators");
     unsigned long long *acc = reinterpret_cast<unsigned long long *>(red + 128);

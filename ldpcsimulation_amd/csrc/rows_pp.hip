@@ -80,6 +80,14 @@ namespace {
 #ifndef LDPC_PP_EXP
 #define LDPC_PP_EXP 0
 #endif
+// Wrong-result timing switches build only into A/B libraries (the *variant targets define
+// LDPC_AB_BUILD); a product build with one of them set is refused.
+#if LDPC_PP_EXP != 0 && !defined(LDPC_AB_BUILD)
+#error "LDPC_PP_EXP != 0 gives wrong results by design: make ppvariant only"
+#endif
+#if LDPC_PP_TAILEXP != 0 && !defined(LDPC_AB_BUILD)
+#error "LDPC_PP_TAILEXP != 0 gives wrong results by design: make ppvariant only"
+#endif
 #ifndef LDPC_PP_BITDELAY
 #define LDPC_PP_BITDELAY 0
 #endif

@@ -27,6 +27,8 @@ OPTIONS = {"rows64": 1, "rows32": 2, "pp_slots": 3, "kernel": 4, "flood_mode": 5
            "layered_bpc": 12, "layered_lds_pos": 13, "layered_rows64": 14, "layered_threads": 15,
            "rows_bpc": 16, "fast_bpc": 17, "bp_kernel": 18, "gdbf_kernel": 19, "ems_threads": 20,
            "ems_swizzle": 21}
+# options of the GF(q) EMS context only (ldpc_nb_ctx_set_option); the binary context refuses them
+EMS_OPTIONS = ("ems_threads", "ems_swizzle")
 # symbolic values of the kernel-choice options
 OPTION_VALUES = {"rows64": {"pp": 0, "fast": 1, "rows": 2}, "rows32": {"pp": 0, "fast": 1, "rows": 2},
                  "pp_slots": {"split": 0, "plain": 1}, "kernel": {"auto": 0, "lds": 1, "flood": 2, "global": 3},
@@ -371,8 +373,8 @@ class Context:
 
     def reset_options(self):
         """Every option back to 0, the library's own kernel choice."""
-        for k in OPTIONS.values():
-            if k not in (20, 21):   # the EMS options belong to the nb context
+        for name, k in OPTIONS.items():
+            if name not in EMS_OPTIONS:   # those belong to the nb context (NbContext.set_options)
                 _check(lib().ldpc_ctx_set_option(self._h, k, 0))
 
     def synchronize(self):

@@ -239,9 +239,10 @@ def _ems_sweep(a, seed, world, rank, device, ck=None) -> int:
             "precision": "f32", "rounds": res.rounds, "frames_decoded": res.frames_decoded}
 
     _run_points(a, ck, rank, bits, run_point)
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized():
-        dist.destroy_process_group()
+    if "WORLD_SIZE" in os.environ:   # a process group exists only under torchrun (torch optional otherwise)
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            dist.destroy_process_group()
     return 0
 
 

@@ -4,7 +4,7 @@
 set -eu
 cd "$(dirname "$0")/.."
 L=ldpcsimulation_amd/lib; V=ab; mkdir -p $V/obj_ppst
-H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Ildpcsimulation_amd/csrc -Wall -Wno-unused-result -DLDPC_STAMPS ${EXTRA:-}"
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude -Ildpcsimulation_amd/csrc -Wall -Wno-unused-result -DLDPC_STAMPS -DLDPC_AB_BUILD ${EXTRA:-}"
 $H -Xclang -target-feature -Xclang -load-store-opt -falign-loops=32 -mllvm -amdgpu-sched-strategy=max-memory-clause \
     -c -o $V/obj_ppst/rows_pp.o ldpcsimulation_amd/csrc/rows_pp.hip 2>/dev/null
 $H -c -o $V/obj_ppst/api.o ldpcsimulation_amd/csrc/api.cpp 2>/dev/null

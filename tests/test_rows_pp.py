@@ -258,3 +258,42 @@ def test_environment_cannot_reroute_the_product(monkeypatch):
     for x, y in zip(a[:3], b[:3]):
         assert np.array_equal(x, y)
     assert a[3].as_dict() == b[3].as_dict()
+
+
+@pytest.mark.gpu
+def test_binary_context_refuses_ems_options_and_orders_stream_changes():
+    """the EMS options (20, 21) belong to the nb context, so the binary context
+    refuses them; reset_options skips them by name. A stream change orders the context's
+    next launch after the previous stream's work (ldpc_ctx_set_stream's event), so two
+    async launches of one context on two streams give the same counts as one stream."""
+    import torch
+    from ldpcsimulation_amd import native
+    ctx = native.Context(native.Graph.from_alist(code_path(CODE)), 0, 4096)
+    for name in native.EMS_OPTIONS:
+        with pytest.raises(native.LdpcError):
+            ctx.set_option(name, 0)
+    ctx.reset_options()
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50, precision=native.F64)
+    ref = ctx.sim_batch(1.5, 0.5, cfg, seed=11, stream_id=0, first_cw=0, batch=4096)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    ctx.read_counts(reset=True)
+    ctx.set_stream(s1.cuda_stream)
+    ctx.sim_launch(1.5, 0.5, cfg, seed=11, stream_id=0, first_cw=0, batch=2048)
+    ctx.set_stream(s2.cuda_stream)
+    ctx.sim_launch(1.5, 0.5, cfg, seed=11, stream_id=0, first_cw=2048, batch=2048)
+    ctx.synchronize()
+    ctx.set_stream(None)
+    got = ctx.read_counts(reset=True)
+    assert got.as_dict() == ref.as_dict()
+    # the GDBF rows kernel hands out codewords from the context's ticket word (cleared per
+    # launch): more codewords than one grid, two launches on two streams
+    gcfg = native.GdbfConfig(T=60)
+    gref = ctx.gdbf_sim_batch(3.5, 0.5, gcfg, seed=3, stream_id=0, first_cw=0, batch=4096)[1]
+    ctx.read_counts(reset=True)
+    ctx.set_stream(s1.cuda_stream)
+    ctx.gdbf_sim_launch(3.5, 0.5, gcfg, seed=3, stream_id=0, first_cw=0, batch=2048)
+    ctx.set_stream(s2.cuda_stream)
+    ctx.gdbf_sim_launch(3.5, 0.5, gcfg, seed=3, stream_id=0, first_cw=2048, batch=2048)
+    ctx.synchronize()
+    ctx.set_stream(None)
+    assert ctx.read_counts(reset=True).as_dict() == gref.as_dict()

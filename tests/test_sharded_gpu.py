@@ -265,3 +265,28 @@ def test_bench_one_rank_rccl_line():
     assert line["collective_backend"] == "nccl" and line["n_gpus"] == 1 and line["steps"] == 2
     assert line["value"] > 0 and line["fer"]["frames"] == 2 * 8192
     assert line["kernel_info"]["kernel"] == "rows_pp"
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_share_device_line():
+    """bench.py's world > 1 branches execute on the MI355X before the
+    driver's 8-GPU run does -- the torchrun child it spawns itself (nothing touched the
+    GPU before), the per-rank `first` offsets, global_batch, the max-over-ranks elapsed
+    and the frames_total == steps * B * world assertion. Two ranks share device 0 and
+    exchange over gloo (the frame sharding of scripts/minsum_example_PEGReg504x1008.sh:23-27
+    replaced by frame-index shards; decodeMinSum.cpp:189's frame loop per shard)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", "--share-device",
+                        "--steps", "2", "--warmup", "1", "--batch", "4096", "--no-cpu-baseline", "--no-secondary",
+                        "--live-pmc", "off"], cwd=root, env=dict(os.environ), capture_output=True, text=True,
+                       timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1   # rank 0 alone prints
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["steps"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["global_batch"] == 8192 and line["config"]["batch_per_gpu"] == 4096
+    assert line["fer"]["frames"] == 2 * 2 * 4096
+    assert line["kernel_info"]["kernel"] == "rows_pp"
+    assert line["collective_backend"] == "gloo"
+    assert line["value"] > 0 and line["ms_per_step"] > 0
