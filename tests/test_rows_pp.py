@@ -274,7 +274,7 @@ def test_binary_context_refuses_ems_options_and_orders_stream_changes():
             ctx.set_option(name, 0)
     ctx.reset_options()
     cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=50, precision=native.F64)
-    ref = ctx.sim_batch(1.5, 0.5, cfg, seed=11, stream_id=0, first_cw=0, batch=4096)
+    ref = ctx.sim_batch(1.5, 0.5, cfg, seed=11, stream_id=0, first_cw=0, batch=4096)[1]
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
     ctx.read_counts(reset=True)
     ctx.set_stream(s1.cuda_stream)
