@@ -60,7 +60,7 @@ $(LIBDIR)/obj/rows_pp.o: $(CSRC)/rows_pp.hip $(CSRC)/fast64.h $(CSRC)/kernels.h 
 	$(HIPCC) $(HIPFLAGS) $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED) -c -o $@ $<
 $(LIBDIR)/obj/gdbf.o: $(CSRC)/gdbf.hip $(CSRC)/gdbf.h $(CSRC)/kernels.h $(CSRC)/device_common.h $(CSRC)/minsum_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(NOSLP) -c -o $@ $<
-$(LIBDIR)/obj/bp.o: $(CSRC)/bp.hip $(CSRC)/bp.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
+$(LIBDIR)/obj/bp.o: $(CSRC)/bp.hip $(CSRC)/bp.h $(CSRC)/bp_math.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 $(LIBDIR)/obj/nb.o: $(CSRC)/nb.hip $(CSRC)/nb.h $(CSRC)/nb_layout.h $(CSRC)/kernels.h $(CSRC)/device_common.h | $(LIBDIR)/obj
 	$(HIPCC) $(HIPFLAGS) $(NOSLP) -c -o $@ $<
@@ -163,6 +163,29 @@ bpvariant: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(VARDIR)/libldpc_hip_$(NAME).so \
 	    $(filter-out $(LIBDIR)/obj/bp.o,$(OBJS)) $(VARDIR)/obj_$(NAME)/bp.o
 
+# Bounds-checked device build (check.h): every schedule-derived LDS / global
+# index of the kernels tested on the device, violations reported by the ABI call that
+# launched them. Same sources and per-file flags as the product, plus -DLDPC_CHECK; a
+# library of its own (tests/test_checked_build.py loads it in a child process).
+CHKDIR    = $(LIBDIR)/checked
+CHKLIB    = $(CHKDIR)/libldpc_hip_checked.so
+CHK_OBJS  = $(patsubst $(LIBDIR)/obj/%.o,$(CHKDIR)/obj/%.o,$(OBJS))
+CHK_HDRS  = $(wildcard $(CSRC)/*.h) include/ldpc_hip.h
+FLAGS_kernels   = $(KERNFLAGS) $(NOSLP)
+FLAGS_rows_fast = $(KERNFLAGS)
+FLAGS_rows_pp   = $(KERNFLAGS) $(ALIGNFLAGS) $(PPSCHED)
+FLAGS_gdbf      = $(NOSLP)
+FLAGS_nb        = $(NOSLP)
+$(CHKDIR)/obj:
+	mkdir -p $@
+$(CHKDIR)/obj/%.o: $(CSRC)/%.hip $(CHK_HDRS) | $(CHKDIR)/obj
+	$(HIPCC) $(HIPFLAGS) $(FLAGS_$*) -DLDPC_CHECK -c -o $@ $<
+$(CHKDIR)/obj/%.o: $(CSRC)/%.cpp $(CHK_HDRS) | $(CHKDIR)/obj
+	$(HIPCC) $(HIPFLAGS) -DLDPC_CHECK -c -o $@ $<
+$(CHKLIB): $(CHK_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(CHK_OBJS)
+checked: $(CHKLIB)
+
 oracle:
 	$(MAKE) -f oracle/Makefile
 
@@ -173,7 +196,7 @@ ref:
 clean:
 	rm -rf $(LIBDIR) $(BINDIR) oracle/liboracle.so
 
-.PHONY: all oracle ref clean clean-ab variant fastvariant ppvariant nbvariant gdbfvariant bpvariant
+.PHONY: all checked oracle ref clean clean-ab variant fastvariant ppvariant nbvariant gdbfvariant bpvariant
 
 # Host-code sanitizer build: graph.cpp (the Tanner-graph compiler), nb_graph.cpp
 # (the NB alist reader, GF tables, slot swizzles), cli_common.h (the CLIs' codeword files)

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LDPC_ABI_VERSION 10
+#define LDPC_ABI_VERSION 11
 
 typedef enum {
     LDPC_OK = 0,
@@ -130,6 +130,19 @@ const char *ldpc_last_error(void);
  * with r = RN(1/alpha) -- exact for alpha = P * 2^E, odd P < 2^20, 2^-900 < alpha
  * <= 2^60 -- else 0 (IEEE division). No device call. */
 int         ldpc_f64_nms_fast_division(double alpha);
+/* (ABI 11) The fp64 BP check node's transcendentals as the device computes
+ * them (bp_math.h: tanh for th_k = tanh(v2c/2) and log for c2v = log((1+p)/(1-p)),
+ * decodeBP.cpp:353-377), evaluated on device `device` for n host values x:
+ * tanh_out[i] = tanh(x[i]), log_out[i] = log(x[i]) (either output may be NULL).
+ * Verification only (tests/test_bp.py measures their ulp distance to glibc). */
+int         ldpc_bp_math_probe(int device, const double *x, int n, double *tanh_out, double *log_out);
+/* (ABI 11) The device bounds checks of the checked build (`make checked`,
+ * ldpcsimulation_amd/lib/checked/libldpc_hip_checked.so; check.h): launches one
+ * kernel that indexes past a bound on purpose and returns what every launch of
+ * that build returns on a violation -- LDPC_ERR_DEVICE, ldpc_last_error() naming
+ * the site, index and bound. The product library compiles no checks and returns
+ * LDPC_ERR_UNSUPPORTED. */
+int         ldpc_check_selftest(int device);
 
 /* ---- graph (H matrix) ------------------------------------------------ */
 /* Arrays exactly as alist_struct (inc/alist.h:21-36): nlist[i] has

@@ -23,6 +23,7 @@
 
 #include "graph.h"
 #include "kernels.h"
+#include "check.h"
 
 static thread_local std::string g_last_error;
 
@@ -46,6 +47,48 @@ static int set_err(int code, const char *fmt, ...)
                            __FILE__, __LINE__);                                                 \
         }                                                                                       \
     } while (0)
+
+#ifdef LDPC_CHECK
+namespace ldpc {
+static const char *check_site_name(unsigned s)
+{
+    static const char *const names[CHK_SITES] = {
+        "?", "rows_pp gather (app entry)", "rows_pp scatter (c2v slot)", "rows_pp bit read (c2v slot)",
+        "rows_pp app write", "rows_fast gather (app entry)", "rows_fast scatter (c2v slot)",
+        "rows_fast bit read (c2v slot)", "rows_fast app write", "flood/layered bit position",
+        "flood c2v / eref slot", "flood packed-state row", "gdbf_rows bit", "gdbf_rows check term slot",
+        "EMS message slot", "bp_rows bit", "bp_rows message slot"};
+    return s < CHK_SITES ? names[s] : "?";
+}
+long check_collect(hipStream_t s, char *msg, size_t msg_len)
+{
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return -(long)e;
+    hipError_t (*const take[])(CheckRec *) = {check_take_rows_pp, check_take_rows_fast, check_take_kernels,
+                                              check_take_gdbf, check_take_nb, check_take_bp};
+    long total = 0;
+    for (auto fn : take) {
+        CheckRec r{};
+        if ((e = fn(&r)) != hipSuccess) return -(long)e;
+        if (r.count && !total)
+            std::snprintf(msg, msg_len, "LDPC_CHECK: %s index %u >= bound %u (block %u, thread %u)",
+                          check_site_name(r.site), r.idx, r.bound, r.block, r.thread);
+        total += r.count;
+    }
+    return total;
+}
+}  // namespace ldpc
+// checked builds: every launch is synchronised and its indices' record read
+#define LDPC_CHECK_AFTER_LAUNCH(stream)                                                              \
+    do {                                                                                             \
+        char m_[192];                                                                                \
+        const long n_ = ldpc::check_collect((stream), m_, sizeof m_);                                \
+        if (n_ < 0) return set_err(LDPC_ERR_DEVICE, "check_collect: %s", hipGetErrorString((hipError_t)-n_)); \
+        if (n_ > 0) return set_err(LDPC_ERR_DEVICE, "%s; %ld violations", m_, n_);                   \
+    } while (0)
+#else
+#define LDPC_CHECK_AFTER_LAUNCH(stream) ((void)0)
+#endif
 
 struct DevBuf {
     void *p = nullptr;
@@ -260,6 +303,45 @@ int ldpc_graph_layers(const ldpc_graph *g, int32_t *row_order, int32_t *layer_pt
 }
 
 // ----------------------------------------------------------------- context
+int ldpc_bp_math_probe(int device, const double *x, int n, double *tanh_out, double *log_out)
+{
+    if (!x || n < 0) return set_err(LDPC_ERR_INVALID, "x is null or n < 0");
+    if (n == 0) return LDPC_OK;
+    HIP_TRY(hipSetDevice(device));
+    const size_t bytes = sizeof(double) * (size_t)n;
+    double *dx = nullptr, *dt = nullptr, *dl = nullptr;
+    hipError_t e = hipMalloc(&dx, 3 * bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(LDPC_ERR_NOMEM, "hipMalloc(%zu): %s", 3 * bytes, hipGetErrorString(e));
+    }
+    dt = dx + n;
+    dl = dt + n;
+    e = hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = ldpc::bp_math_probe(dx, tanh_out ? dt : nullptr, log_out ? dl : nullptr, n, nullptr);
+    if (e == hipSuccess && tanh_out) e = hipMemcpy(tanh_out, dt, bytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && log_out) e = hipMemcpy(log_out, dl, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(dx);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return set_err(LDPC_ERR_DEVICE, "bp math probe: %s", hipGetErrorString(e));
+    }
+    return LDPC_OK;
+}
+
+int ldpc_check_selftest(int device)
+{
+#ifdef LDPC_CHECK
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(ldpc::check_selftest_launch(nullptr));
+    LDPC_CHECK_AFTER_LAUNCH(nullptr);
+    return set_err(LDPC_ERR_DEVICE, "LDPC_CHECK self-test: the violation was not recorded");
+#else
+    (void)device;
+    return set_err(LDPC_ERR_UNSUPPORTED, "this library has no device index checks (build `make checked`)");
+#endif
+}
+
 int ldpc_device_count(int *n)
 {
     if (!n) return set_err(LDPC_ERR_INVALID, "n is null");
@@ -670,6 +752,7 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         HIP_TRY(ldpc::bp_launch(c->dg, a, f64, kc, c->gscratch.p, gblocks, c->g->E, c->num_cus, c->stream));
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
         c->timed = true;
+        LDPC_CHECK_AFTER_LAUNCH(c->stream);
         return LDPC_OK;
     }
     int gblocks = layered ? c->num_cus : 0;
@@ -737,8 +820,10 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         }
     }
 #endif
+    LDPC_CHECK_AFTER_LAUNCH(c->stream);
     return LDPC_OK;
 }
+
 
 static int read_counts(ldpc_ctx *c, ldpc_counts *out, int reset)
 {
@@ -1133,6 +1218,7 @@ static int gdbf_run(ldpc_ctx *c, const ldpc::GdbfArgs &a, bool f64)
     HIP_TRY(ldpc::gdbf_launch(c->dg, a, f64, ch, c->gscratch.p, slots, c->num_cus, c->stream));
     HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+    LDPC_CHECK_AFTER_LAUNCH(c->stream);
     return LDPC_OK;
 }
 

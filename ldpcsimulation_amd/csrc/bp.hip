@@ -10,10 +10,11 @@
 // and c2v[M][dcs] (by row and mlist position); v2c is not stored: the check
 // node rebuilds it as clip(app - c2v_old), the same IEEE subtraction and
 // clip the reference's bit node performs. State in LDS when it fits, else in
-// a global slot. tanh/log are the device's (OCML), so messages agree with the
-// glibc reference to a few ulp, not bit for bit: parity is by tolerance and
-// by FER (tests/test_bp.py).
+// a global slot. tanh/log are the device's (fp64: bp_math.h, branch-free argument
+// reduction + polynomial; fp32: OCML), so messages agree with the glibc reference
+// to a few ulp, not bit for bit: parity is by tolerance and by FER (tests/test_bp.py).
 #include "bp.h"
+#include "bp_math.h"
 #include "device_common.h"
 
 #include <hip/hip_runtime.h>
@@ -23,9 +24,24 @@
 namespace ldpc {
 
 __device__ __forceinline__ float bp_tanh(float x) { return tanhf(x); }
-__device__ __forceinline__ double bp_tanh(double x) { return tanh(x); }
+__device__ __forceinline__ double bp_tanh(double x) { return bp_tanh64(x); }   // bp_math.h
 __device__ __forceinline__ float bp_log(float x) { return logf(x); }
-__device__ __forceinline__ double bp_log(double x) { return log(x); }
+__device__ __forceinline__ double bp_log(double x) { return bp_log64(x); }     // bp_math.h
+
+__global__ __launch_bounds__(256) void k_bp_math_probe(const double *x, double *t, double *l, int n)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    if (t) t[i] = bp_tanh(x[i]);
+    if (l) l[i] = bp_log(x[i]);
+}
+
+hipError_t bp_math_probe(const double *x, double *t, double *l, int n, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bp_math_probe, dim3((n + 255) / 256), dim3(256), 0, s, x, t, l, n);
+    return hipGetLastError();
+}
 template <typename F> __device__ __forceinline__ F bp_abs(F x) { return x < F(0) ? -x : x; }
 
 template <typename F, int SRC, int DCB>
@@ -261,11 +277,15 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
         }
     __syncthreads();
     uint32_t rc[RPT][DC / 2], rp[RPT][DC / 2];
-    int rdeg[RPT];
+    int rdeg[RPT], wmax[RPT];   // wmax: the wave's largest degree of row slot r (wave-uniform)
 #pragma unroll
     for (int r = 0; r < RPT; ++r) {
         const int j = tid + r * NT;
         rdeg[r] = j < M ? g.row_deg[j] : 0;
+        int m = rdeg[r];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        wmax[r] = __builtin_amdgcn_readfirstlane(m);
 #pragma unroll
         for (int k = 0; k < DC; k += 2) {
             const uint32_t c0 = k < rdeg[r] ? (uint32_t)g.row_cols[(size_t)j * g.dcs + k] : (uint32_t)N;
@@ -348,12 +368,19 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
 #pragma unroll
             for (int r = 0; r < RPT; ++r) {
                 if (LDPC_BP_PRIOBAL && r > 0) __builtin_amdgcn_s_setprio(2);
+                // fp64: edges and outputs past the wave's largest row degree are skipped (an
+                // SGPR branch): th = 1 there, as for a padding edge of a lower-degree row (fp32
+                // keeps the straight-line row: 10.3 vs 11.3 ms with the branches)
                 F th[DC];
 #pragma unroll
                 for (int k = 0; k < DC; ++k) {
-                    F v = app[(rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu] - prev[r][k];   // :399
-                    if (bp_abs(v) > maxllr) v = maxllr * (v >= F(0) ? F(1) : F(-1));      // :400-401
-                    th[k] = k < rdeg[r] ? bp_tanh(v / F(2)) : F(1);
+                    th[k] = F(1);
+                    if (sizeof(F) == 4 || k < wmax[r]) {
+                        F v = app[LDPC_CHK((rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu, (uint32_t)N + 1, CHK_BP_COL)] -
+                              prev[r][k];   // :399
+                        if (bp_abs(v) > maxllr) v = maxllr * (v >= F(0) ? F(1) : F(-1));      // :400-401
+                        th[k] = k < rdeg[r] ? bp_tanh(v / F(2)) : F(1);
+                    }
                 }
                 // prod over k != jj in mlist order from 1 (:362-371): its first jj factors
                 // are the running prefix pre[jj] -- the same roundings -- so only the
@@ -364,13 +391,14 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
                 for (int k = 0; k + 1 < DC; ++k) pre[k + 1] = pre[k] * th[k];
 #pragma unroll
                 for (int jj = 0; jj < DC; ++jj) {
+                    if (sizeof(F) == 8 && jj >= wmax[r]) continue;
                     F prod = pre[jj];
 #pragma unroll
                     for (int k = jj + 1; k < DC; ++k) prod *= th[k];
                     F o = bp_log((F(1) + prod) / (F(1) - prod));
                     if (sizeof(F) == 4 && bp_abs(o) > maxllr) o = o >= F(0) ? maxllr : -maxllr;
                     prev[r][jj] = o;
-                    if (jj < rdeg[r]) msg[(rp[r][jj / 2] >> (16 * (jj & 1))) & 0xffffu] = o;
+                    if (jj < rdeg[r]) msg[LDPC_CHK((rp[r][jj / 2] >> (16 * (jj & 1))) & 0xffffu, (uint32_t)E + 1, CHK_BP_MSG)] = o;
                 }
             }
             if (LDPC_BP_PRIOBAL) __builtin_amdgcn_s_setprio(0);
@@ -380,7 +408,7 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     F sum = yq[q];
-                    for (int k = 0; k < wdeg; ++k) sum += msg[k < deg[q] ? e0[q] + k : E];
+                    for (int k = 0; k < wdeg; ++k) sum += msg[LDPC_CHK(k < deg[q] ? e0[q] + k : E, E + 1, CHK_BP_MSG)];
                     if (v0 + q < N) app[v0 + q] = sum;
                 }
             }
@@ -407,7 +435,7 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
 #pragma unroll
             for (int k = 0; k < DC; ++k)
                 if (k < rdeg[r]) {
-                    const F s = app[(rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu];
+                    const F s = app[LDPC_CHK((rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu, (uint32_t)N + 1, CHK_BP_COL)];
                     par ^= a.T > 0 ? (s > F(0) ? 0 : 1) : (s >= F(0) ? 0 : 1);
                 }
             synd |= par;
@@ -428,6 +456,22 @@ __global__ __launch_bounds__(NT, NT == 512 && sizeof(F) == 4 ? LDPC_BP_ROWS_WAVE
         __syncthreads();
     }
 }
+
+LDPC_CHECK_TU(bp)
+
+#ifdef LDPC_CHECK
+__global__ void k_check_selftest(int *sink)
+{
+    // entry 7 of a 3-entry table: recorded (site CHK_BP_COL) and clamped to 0
+    const int i = LDPC_CHK(threadIdx.x + 7, 3, CHK_BP_COL);
+    if (sink) sink[i] = 1;
+}
+hipError_t check_selftest_launch(hipStream_t s)
+{
+    hipLaunchKernelGGL(k_check_selftest, dim3(1), dim3(1), 0, s, (int *)nullptr);
+    return hipGetLastError();
+}
+#endif
 
 static bool bp_rows_forced_off() { return opt(LDPC_OPT_BP_KERNEL) == 1; }
 

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "check.h"
+
 namespace ldpc {
 
 // ---------------------------------------------------------------------

@@ -189,6 +189,21 @@ __device__ __forceinline__ uint32_t addr8(const uint32_t (&w)[DC / 2], int k, ui
         asm("v_mad_u32_u16 %0, %1, 8, %2" : "=v"(a) : "v"(w[k >> 1]), "v"(base));
     return a;
 }
+// LDPC_ADDR8(DC, w, k, base, n, site): addr8 with the entry bounds-checked (entry < n)
+// in LDPC_CHECK builds (check.h); in the product build exactly addr8<DC>(w, k, base)
+// (n and site are not evaluated).
+#ifdef LDPC_CHECK
+template <int DC>
+__device__ __forceinline__ uint32_t addr8c(const uint32_t (&w)[DC / 2], int k, uint32_t base, uint32_t n,
+                                           unsigned site)
+{
+    const uint32_t e = (w[k >> 1] >> ((k & 1) * 16)) & 0xffffu;
+    return base + 8u * LDPC_CHK(e, n, site);
+}
+#define LDPC_ADDR8(DC, w, k, base, n, site) addr8c<DC>(w, k, base, n, site)
+#else
+#define LDPC_ADDR8(DC, w, k, base, n, site) addr8<DC>(w, k, base)
+#endif
 // LDS accesses by 32-bit LDS address (no generic-pointer arithmetic: the
 // address from addr8 goes straight into the ds_read / ds_write).
 __device__ __forceinline__ uint32_t lds_addr_of(const void *p)

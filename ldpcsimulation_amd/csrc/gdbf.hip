@@ -566,7 +566,8 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
 #pragma unroll
             for (int r = 0; r < RPT; ++r)
 #pragma unroll
-                for (int k = 0; k < DC; ++k) g8[r][k] = dl[(rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu];
+                for (int k = 0; k < DC; ++k)
+                    g8[r][k] = dl[LDPC_CHK((rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu, (uint32_t)np, CHK_GDBF_BIT)];
             F pv[BPT];
 #pragma unroll
             for (int q = 0; q < BPT; ++q) pv[q] = F(0);
@@ -595,7 +596,8 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
                 uint32_t p = 0;
 #pragma unroll
                 for (int k = 0; k < DC; ++k) p ^= g8[r][k];
-                if (rvalid[r]) sl[sidx(tid + r * NT)] = w * (p ? F(-1) : F(1));   // w * (F)s_j, as :541-551 adds it
+                if (rvalid[r])
+                    sl[LDPC_CHK(sidx(tid + r * NT), sidx(M) + 1, CHK_GDBF_CHECK)] = w * (p ? F(-1) : F(1));   // w * (F)s_j, as :541-551 adds it
                 fail |= (int)p;
             }
             if (fail) fl[it & 1] = 1;
@@ -617,14 +619,16 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
                 constexpr int K0 = DVM < 4 ? DVM : 4;
                 F sv[K0];
 #pragma unroll
-                for (int k = 0; k < K0; ++k) sv[k] = sl[(bc[q][k / 2] >> (16 * (k & 1))) & 0xffffu];
+                for (int k = 0; k < K0; ++k)
+                    sv[k] = sl[LDPC_CHK((bc[q][k / 2] >> (16 * (k & 1))) & 0xffffu, sidx(M) + 1, CHK_GDBF_CHECK)];
                 F E = (F)d[q] * yq[q];
 #pragma unroll
                 for (int k = 0; k < K0; ++k) E += sv[k];
                 if (DVM > K0 && wdeg[q] > K0) {
                     F sw[DVM - K0 > 0 ? DVM - K0 : 1];
 #pragma unroll
-                    for (int k = K0; k < DVM; ++k) sw[k - K0] = sl[(bc[q][k / 2] >> (16 * (k & 1))) & 0xffffu];
+                    for (int k = K0; k < DVM; ++k)
+                        sw[k - K0] = sl[LDPC_CHK((bc[q][k / 2] >> (16 * (k & 1))) & 0xffffu, sidx(M) + 1, CHK_GDBF_CHECK)];
 #pragma unroll
                     for (int k = K0; k < DVM; ++k)
                         if (k < wdeg[q]) E += sw[k - K0];
@@ -665,7 +669,7 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
         for (int r = 0; r < RPT; ++r) {
             uint32_t p = 0;
 #pragma unroll
-            for (int k = 0; k < DC; ++k) p ^= dl[(rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu];
+            for (int k = 0; k < DC; ++k) p ^= dl[LDPC_CHK((rc[r][k / 2] >> (16 * (k & 1))) & 0xffffu, (uint32_t)np, CHK_GDBF_BIT)];
             synd |= (int)p;
         }
         int sums[3] = {wgt, unc, synd};
@@ -694,6 +698,8 @@ __global__ __launch_bounds__(NT, NT != 512 ? 4 : sizeof(F) == 4 ? LDPC_GDBF_ROWS
 
 constexpr size_t kGdbfMaxLds = 64 * 1024;
 constexpr int kGdbfRowsUnsupported = GDBF_SEQUENTIAL | GDBF_MODESWITCH | GDBF_QPROB;
+
+LDPC_CHECK_TU(gdbf)
 
 static bool gdbf_rows_forced_off() { return opt(LDPC_OPT_GDBF_KERNEL) == 1; }
 

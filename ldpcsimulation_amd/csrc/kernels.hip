@@ -554,7 +554,7 @@ __global__ __launch_bounds__(256) void k_flood_init(DecodeArgs a, DevGraph g, Fl
             const int v = t * 4 + q;
             if (v < N) {
                 const F q2 = front_end<F>(yv[q], a);
-                const int p = fs.pos_of_bit[v];
+                const int p = LDPC_CHK(fs.pos_of_bit[v], NP, CHK_FLOOD_APP);
                 S.yq[p] = q2;
                 S.app[p] = q2;
                 const int cv = cvec ? cvec[v] : 1;
@@ -689,8 +689,8 @@ __global__ __launch_bounds__(256) void k_flood_check(DecodeArgs a, FloodSched fs
     int sp[DC], sq[DC];
 #pragma unroll
     for (int k = 0; k < DC; ++k) {
-        sp[k] = k < deg ? fs.sp[(size_t)k * MP + i] : NP;
-        sq[k] = k < deg ? fs.sq[(size_t)k * MP + i] : 0;
+        sp[k] = k < deg ? LDPC_CHK(fs.sp[(size_t)k * MP + i], NP + 1, CHK_FLOOD_APP) : NP;
+        sq[k] = k < deg ? LDPC_CHK(fs.sq[(size_t)k * MP + i], fs.e_pad + 64, CHK_FLOOD_C2V) : 0;
     }
     for (int r = r0; r < nres; r += SPS * rs) {
         F xa[SPS][DC];
@@ -730,12 +730,13 @@ __global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char 
     const int d = fs.pdeg[p];
     if (d == 0) return;
     const int off = fs.gbase[p >> 6] + (p & 63);
+    [[maybe_unused]] const int ea = fs.e_pad + 64;
     if constexpr (DV == 0) {
         for (int r = r0; r < nres; r += rs) {
             const auto S = FloodSlot::at<F>(scratch, slot_bytes, r, fs);
             const F *cp = S.c2v + off;
             F sum = S.yq[p];
-            for (int e = 0; e < d; ++e) sum += cp[64 * e];   // nlist order (:452-476)
+            for (int e = 0; e < d; ++e) sum += cp[LDPC_CHK(64 * e, ea - off, CHK_FLOOD_C2V)];   // nlist order (:452-476)
             S.app[p] = sum;
         }
     } else {
@@ -746,7 +747,7 @@ __global__ __launch_bounds__(256) void k_flood_bit(FloodSched fs, unsigned char 
                 const auto S = FloodSlot::at<F>(scratch, slot_bytes, r + j * rs < nres ? r + j * rs : r, fs);
                 y[j] = S.yq[p];
 #pragma unroll
-                for (int e = 0; e < DV; ++e) v[j][e] = e < d ? S.c2v[off + 64 * e] : F(0);
+                for (int e = 0; e < DV; ++e) v[j][e] = e < d ? S.c2v[LDPC_CHK(off + 64 * e, ea, CHK_FLOOD_C2V)] : F(0);
             }
 #pragma unroll
             for (int j = 0; j < SPS; ++j) {
@@ -783,7 +784,12 @@ __global__ __launch_bounds__(256) void k_flood_bit_packed(FloodSched fs, unsigne
     const int off = fs.gbase[p >> 6] + (p & 63);
     uint32_t ref[DV];
 #pragma unroll
-    for (int e = 0; e < DV; ++e) ref[e] = e < d ? fs.eref[off + 64 * e] : 0u;
+    for (int e = 0; e < DV; ++e) {
+        ref[e] = e < d ? fs.eref[LDPC_CHK(off + 64 * e, fs.e_pad + 64, CHK_FLOOD_C2V)] : 0u;
+#ifdef LDPC_CHECK
+        ref[e] = (LDPC_CHK(ref[e] >> 5, (uint32_t)fs.M_pad, CHK_FLOOD_ROW) << 5) | (ref[e] & 31u);
+#endif
+    }
     for (int r = r0; r < nres; r += SPS * rs) {
         F2 m[SPS][DV];
         uint32_t me[SPS][DV];
@@ -830,13 +836,14 @@ __global__ __launch_bounds__(256) void k_flood_finish(DecodeArgs a, DevGraph g, 
             } else if (a.cw_table) {
                 cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
             }
-            const int d = S.app[fs.pos_of_bit[t]] > F(0) ? 1 : -1;   // :471-474
+            const int d = S.app[LDPC_CHK(fs.pos_of_bit[t], fs.ngroups * 64 + 1, CHK_FLOOD_APP)] > F(0) ? 1 : -1;   // :471-474
             w = d != (cvec ? cvec[t] : 1);
             if (a.d_out) a.d_out[(size_t)b * N + t] = (int8_t)d;
         }
         if (t < MP) {
             const int deg = fs.rdeg[t];
-            for (int k = 0; k < deg; ++k) par ^= (S.app[fs.sp[(size_t)k * MP + t]] > F(0)) ? 0 : 1;
+            for (int k = 0; k < deg; ++k)
+                par ^= (S.app[LDPC_CHK(fs.sp[(size_t)k * MP + t], fs.ngroups * 64 + 1, CHK_FLOOD_APP)] > F(0)) ? 0 : 1;
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -1146,7 +1153,8 @@ struct LayApp {
 
 template <typename F, int SRC, bool SPLIT>
 __device__ __forceinline__ int channel_to_storage(const DecodeArgs &a, const DevGraph &g, const LayerSched &ls,
-                                                  int b, const int8_t *cvec, const LayApp<F, SPLIT> &app)
+                                                  int b, const int8_t *cvec, const LayApp<F, SPLIT> &app,
+                                                  [[maybe_unused]] int np1)
 {
     const int tid = threadIdx.x, nt = blockDim.x, N = g.N;
     const uint64_t cw = a.first_cw + (uint64_t)b;
@@ -1155,7 +1163,7 @@ __device__ __forceinline__ int channel_to_storage(const DecodeArgs &a, const Dev
         const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
         for (int v = tid; v < N; v += nt) {
             const F q = front_end<F>(y[v], a);
-            app.st(ls.pos_of_bit[v], q);
+            app.st(LDPC_CHK(ls.pos_of_bit[v], np1, CHK_FLOOD_APP), q);
             const int cv = cvec ? cvec[v] : 1;
             unc += ((q > F(0) ? 1 : -1) * cv < 0);
         }
@@ -1176,7 +1184,7 @@ __device__ __forceinline__ int channel_to_storage(const DecodeArgs &a, const Dev
                     const F yv = (F)cv * (F(1) + sigma * n[q4]);
                     if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
                     const F q = front_end<F>(yv, a);
-                    app.st(ls.pos_of_bit[v], q);
+                    app.st(LDPC_CHK(ls.pos_of_bit[v], np1, CHK_FLOOD_APP), q);
                     unc += ((q > F(0) ? 1 : -1) * cv < 0);
                 }
             }
@@ -1256,7 +1264,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
         cvec = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
     }
     // ---- channel + front-end (:214-238): app = yq in storage order ----
-    const int unc = channel_to_storage<F, SRC, SPLIT>(a, g, ls, b, cvec, app);
+    const int unc = channel_to_storage<F, SRC, SPLIT>(a, g, ls, b, cvec, app, NP + 1);
     for (int i = tid; i < MP; i += nt) {   // c2v_old = +0 (:364-370)
         F2 z;
         z.x = F(0);
@@ -1281,7 +1289,8 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) sp[r][k] = k < deg[r] ? ls.sp[(size_t)k * MP + i0 + r * nt] : NP;
+                    for (int k = 0; k < DC; ++k)
+                        sp[r][k] = k < deg[r] ? LDPC_CHK(ls.sp[(size_t)k * MP + i0 + r * nt], NP + 1, CHK_FLOOD_APP) : NP;
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -1313,7 +1322,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
     // ---- decisions, error weight (:270, :382-393), syndrome ----
     int w = 0, synd = 0;
     for (int v = tid; v < N; v += nt) {
-        const int d = app.ld(ls.pos_of_bit[v]) > F(0) ? 1 : -1;   // :471-474
+        const int d = app.ld(LDPC_CHK(ls.pos_of_bit[v], NP + 1, CHK_FLOOD_APP)) > F(0) ? 1 : -1;   // :471-474
         const int cv = cvec ? cvec[v] : 1;
         w += (d != cv);
         if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
@@ -1321,7 +1330,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
     for (int i = tid; i < MP; i += nt) {
         const int deg = ls.rdeg[i];
         int par = 0;
-        for (int k = 0; k < deg; ++k) par ^= (app.ld(ls.sp[(size_t)k * MP + i]) > F(0)) ? 0 : 1;
+        for (int k = 0; k < deg; ++k) par ^= (app.ld(LDPC_CHK(ls.sp[(size_t)k * MP + i], NP + 1, CHK_FLOOD_APP)) > F(0)) ? 0 : 1;
         synd |= par;
     }
     int sums[3] = {w, unc, synd};
@@ -1807,6 +1816,8 @@ __global__ __launch_bounds__(256) void k_verify_div(float alpha, float rcp, unsi
     for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o, 64);
     if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(bad, nbad);
 }
+
+LDPC_CHECK_TU(kernels)
 
 hipError_t verify_div_by_reciprocal(float alpha, float rcp, unsigned long long *bad, hipStream_t s)
 {

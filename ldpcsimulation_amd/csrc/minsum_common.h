@@ -133,13 +133,18 @@ __device__ __forceinline__ void padd(Pack<F, C> &s, const Pack<F, C> &r)
 #ifndef LDPC_VN_PIPE
 #define LDPC_VN_PIPE 0
 #endif
+// lim / site: the bound of the slot index base[i] + k*64 relative to c2v and the check
+// site, for LDPC_CHECK builds (check.h); unused otherwise.
 template <typename F, int C, int NACT, int U, int CPT>
-__device__ __forceinline__ void vn_load(const Pack<F, C> *c2v, const int (&base)[CPT], int k, Pack<F, C> (&r)[NACT][U])
+__device__ __forceinline__ void vn_load(const Pack<F, C> *c2v, const int (&base)[CPT], int k, Pack<F, C> (&r)[NACT][U],
+                                        int lim, unsigned site)
 {
+    (void)lim;
+    (void)site;
 #pragma unroll
     for (int i = 0; i < NACT; ++i)
 #pragma unroll
-        for (int u = 0; u < U; ++u) r[i][u] = c2v[base[i] + (k + u) * 64];
+        for (int u = 0; u < U; ++u) r[i][u] = c2v[LDPC_CHK(base[i] + (k + u) * 64, lim, site)];
 }
 template <typename F, int C, int NACT, int U, int CPT, bool PK = false>
 __device__ __forceinline__ void vn_add(const Pack<F, C> (&r)[NACT][U], Pack<F, C> (&sum)[CPT])
@@ -151,21 +156,23 @@ __device__ __forceinline__ void vn_add(const Pack<F, C> (&r)[NACT][U], Pack<F, C
 }
 template <typename F, int C, int NACT, int CPT, bool PK = false>
 __device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base)[CPT], int &k, int kend,
-                                         Pack<F, C> (&sum)[CPT])
+                                         Pack<F, C> (&sum)[CPT], int lim, unsigned site)
 {
+    (void)lim;
+    (void)site;
     constexpr int U = NACT >= 3 ? LDPC_VN_U3 : LDPC_VN_U1;   // packs in flight per step: U * NACT
     if constexpr (LDPC_VN_PIPE) {
         // two steps in flight: step s+1's reads are issued before step s is added
         int n = (kend - k) / U;   // wave-uniform
         if (n > 0) {
             Pack<F, C> ra[NACT][U], rb[NACT][U];
-            vn_load<F, C, NACT, U, CPT>(c2v, base, k, ra);
+            vn_load<F, C, NACT, U, CPT>(c2v, base, k, ra, lim, site);
             for (;;) {
-                if (n >= 2) vn_load<F, C, NACT, U, CPT>(c2v, base, k + U, rb);
+                if (n >= 2) vn_load<F, C, NACT, U, CPT>(c2v, base, k + U, rb, lim, site);
                 vn_add<F, C, NACT, U, CPT, PK>(ra, sum);
                 k += U;
                 if (--n == 0) break;
-                if (n >= 2) vn_load<F, C, NACT, U, CPT>(c2v, base, k + U, ra);
+                if (n >= 2) vn_load<F, C, NACT, U, CPT>(c2v, base, k + U, ra, lim, site);
                 vn_add<F, C, NACT, U, CPT, PK>(rb, sum);
                 k += U;
                 if (--n == 0) break;
@@ -177,7 +184,7 @@ __device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base
 #pragma unroll
         for (int i = 0; i < NACT; ++i)
 #pragma unroll
-            for (int u = 0; u < U; ++u) r[i][u] = c2v[base[i] + (k + u) * 64];
+            for (int u = 0; u < U; ++u) r[i][u] = c2v[LDPC_CHK(base[i] + (k + u) * 64, lim, site)];
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -186,17 +193,17 @@ __device__ __forceinline__ void vn_phase(const Pack<F, C> *c2v, const int (&base
     for (; k < kend; ++k) {
         Pack<F, C> r[NACT];
 #pragma unroll
-        for (int i = 0; i < NACT; ++i) r[i] = c2v[base[i] + k * 64];
+        for (int i = 0; i < NACT; ++i) r[i] = c2v[LDPC_CHK(base[i] + k * 64, lim, site)];
 #pragma unroll
         for (int i = 0; i < NACT; ++i) padd<PK>(sum[i], r[i]);
     }
 }
 template <typename F, int C, int NACT, int CPT, bool PK = false>
 __device__ __forceinline__ void vn_phases(const Pack<F, C> *c2v, const int (&base)[CPT], const int (&gd)[CPT], int &k,
-                                          Pack<F, C> (&sum)[CPT])
+                                          Pack<F, C> (&sum)[CPT], int lim = 0x7fffffff, unsigned site = 0)
 {
-    vn_phase<F, C, NACT, CPT, PK>(c2v, base, k, gd[NACT - 1], sum);
-    if constexpr (NACT > 1) vn_phases<F, C, NACT - 1, CPT, PK>(c2v, base, gd, k, sum);
+    vn_phase<F, C, NACT, CPT, PK>(c2v, base, k, gd[NACT - 1], sum, lim, site);
+    if constexpr (NACT > 1) vn_phases<F, C, NACT - 1, CPT, PK>(c2v, base, gd, k, sum, lim, site);
 }
 
 // Check node, fast fp32 path (MS, and NMS with a verified reciprocal). Exact

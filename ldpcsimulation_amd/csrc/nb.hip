@@ -114,6 +114,7 @@ __device__ __forceinline__ int gf16_xt(int v) { return ((v << 1) & 15) ^ ((v & 8
 template <int Q>
 __device__ __forceinline__ void load_vec(const float *msg, int Ep, int slot, float (&v)[Q])
 {
+    slot = LDPC_CHK(slot, Ep, CHK_EMS_SLOT);
 #pragma unroll
     for (int c = 0; c < Q / 4; ++c) {
         const float4 t = *reinterpret_cast<const float4 *>(msg + ((c * Ep + (slot ^ c)) << 2));
@@ -163,6 +164,7 @@ __device__ __forceinline__ void ecn_reg(const float (&P)[Q], const float (&R)[Q]
 template <int Q>
 __device__ __forceinline__ void store_out(float *msg, int Ep, int slot, float (&w)[Q], int nm, float offset)
 {
+    slot = LDPC_CHK(slot, Ep, CHK_EMS_SLOT);
     if (nm < Q) {
         float mx = -1.0f;
 #pragma unroll
@@ -263,7 +265,7 @@ __device__ __forceinline__ void cn_lane(float *msg, int Ep, int M, int j, int di
 template <int DC>
 __device__ __forceinline__ void syndrome_edge(int M, int s, int hv, int d, uint32_t *synd)
 {
-    int j = s;
+    int j = LDPC_CHK(s, M * DC, CHK_EMS_SLOT);
 #pragma unroll
     for (int k = 1; k < DC; ++k) j -= j >= M ? M : 0;
     const int h1 = hv & 15, h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
@@ -320,6 +322,7 @@ struct MsgAddr {
     __device__ int lam(int p) const { return (p << 2) ^ ((p >> 2) << sh); }
     __device__ void edge(int s, int hv, int (&ad)[Q]) const
     {
+        s = LDPC_CHK(s, 1 << (sh - 4), CHK_EMS_SLOT);   // slots [0, Ep)
         const int h1 = hv & 15, f = hv >> 4;
         const int h2 = gf16_xt(h1), h4 = gf16_xt(h2), h8 = gf16_xt(h4);
         const int L[4] = {lam(h1), lam(h2), lam(h4), lam(h8)};
@@ -776,6 +779,8 @@ NbChoice nb_choose(const NbDevGraph &g, int maxdc)
     }
     return ch;
 }
+
+LDPC_CHECK_TU(nb)
 
 template <int DC, int SRC, bool GS>
 static hipError_t launch_t(const NbDevGraph &g, const NbArgs &a, const NbChoice &ch, void *scratch, int grid,

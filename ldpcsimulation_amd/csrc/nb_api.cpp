@@ -5,6 +5,7 @@
 #include "ldpc_hip.h"
 #include "nb.h"
 #include "nb_graph.h"
+#include "check.h"
 #include "kernels.h"
 
 #include <hip/hip_runtime.h>
@@ -300,6 +301,14 @@ static int run(ldpc_nb_ctx *c, const ldpc::NbArgs &a)
     NB_HIP_TRY(ldpc::nb_launch(dg, a, ch, c->scratch.p, slots, c->num_cus, c->stream));
     NB_HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->timed = true;
+#ifdef LDPC_CHECK
+    {   // checked builds: the launch's index record (check.h)
+        char m[192];
+        const long n = ldpc::check_collect(c->stream, m, sizeof m);
+        if (n < 0) return err(LDPC_ERR_DEVICE, "check_collect: %s", hipGetErrorString((hipError_t)-n));
+        if (n > 0) return err(LDPC_ERR_DEVICE, "%s; %ld violations", m, n);
+    }
+#endif
     return LDPC_OK;
 }
 

@@ -205,14 +205,14 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
         bool in_ok = true;
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
-            const P st = c2v[vdst(i) <= N ? vdst(i) : 0];
+            const P st = c2v[LDPC_CHK(vdst(i) <= N ? vdst(i) : 0, N + 2, CHK_FAST_APP_WRITE)];
             // yq + 0 maps -0 to +0, so app is never -0 (see the header)
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 yq[i].v[c] = st.v[c] + F(0);
                 in_ok &= dabs(yq[i].v[c]) < kMax;
             }
-            app[vdst(i)] = yq[i];   // v2c = yq on the first pass (:364-370)
+            app[LDPC_CHK(vdst(i), N + 2, CHK_FAST_APP_WRITE)] = yq[i];   // v2c = yq on the first pass (:364-370)
         }
         if (!in_ok) red[31] = 1;
         __syncthreads();
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             P z;
 #pragma unroll
             for (int c = 0; c < C; ++c) z.v[c] = F(0);
-            for (int k = dg; k < gd; ++k) c2v[base + k * 64] = z;
+            for (int k = dg; k < gd; ++k) c2v[LDPC_CHK(base + k * 64, EA, CHK_FAST_BIT_READ)] = z;
         }
         P prev[RPT][DC];   // c2v sent on each edge last iteration: +0 before the first
 #pragma unroll
@@ -251,17 +251,22 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             if (LDPC_FAST_PRIOBAL) __builtin_amdgcn_s_setprio(3);
             P xin[LDPC_FAST_PREFETCH ? 2 : 1][DC];
 #pragma unroll
-            for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(LDPC_FAST_EXP == 5 ? app_base + 8 * k : addr8<DC>(colw[0], k, app_base));
+            for (int k = 0; k < DC; ++k)
+                xin[0][k] = lds_at<P>(LDPC_FAST_EXP == 5 ? app_base + 8 * k
+                                                         : LDPC_ADDR8(DC, colw[0], k, app_base, N + 2, CHK_FAST_GATHER));
 #pragma unroll
             for (int r = 0; r < RPT; ++r) {
                 constexpr int NB = LDPC_FAST_PREFETCH ? 2 : 1;
                 if (LDPC_FAST_PREFETCH && r + 1 < RPT) {
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) xin[(r + 1) % NB][k] = lds_at<P>(LDPC_FAST_EXP == 5 ? app_base + 8 * k : addr8<DC>(colw[r + 1 < RPT ? r + 1 : r], k, app_base));
+                    for (int k = 0; k < DC; ++k)
+                        xin[(r + 1) % NB][k] = lds_at<P>(
+                            LDPC_FAST_EXP == 5 ? app_base + 8 * k
+                                               : LDPC_ADDR8(DC, colw[r + 1 < RPT ? r + 1 : r], k, app_base, N + 2, CHK_FAST_GATHER));
                 }
                 if (!LDPC_FAST_PREFETCH && r > 0) {
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(addr8<DC>(colw[r], k, app_base));
+                    for (int k = 0; k < DC; ++k) xin[0][k] = lds_at<P>(LDPC_ADDR8(DC, colw[r], k, app_base, N + 2, CHK_FAST_GATHER));
                 }
                 bool ok;
                 if constexpr (LDPC_FAST_EXP == 4) {
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                 }
                 if constexpr (LDPC_FAST_EXP != 1) {
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) lds_put<P>(addr8<DC>(posw[r], k, c2v_base), prev[r][k]);
+                    for (int k = 0; k < DC; ++k) lds_put<P>(LDPC_ADDR8(DC, posw[r], k, c2v_base, EA, CHK_FAST_SCATTER), prev[r][k]);
                 }
                 if (RPT > 1) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
             }
@@ -301,9 +306,9 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                 // the lane id recomputed here (v_mbcnt), so the lane's c2v pointer is not a
                 // loop-long live value (it was spilled)
                 const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-                vn_phases<F, C, CPT, CPT>(c2v + ln, vgb, vgd, k, sum);
+                vn_phases<F, C, CPT, CPT>(c2v + ln, vgb, vgd, k, sum, LDPC_CHK_LIM(EA - ln), CHK_FAST_BIT_READ);
 #pragma unroll
-                for (int i = 0; i < CPT; ++i) app[vdst(i)] = sum[i];
+                for (int i = 0; i < CPT; ++i) app[LDPC_CHK(vdst(i), N + 2, CHK_FAST_APP_WRITE)] = sum[i];
             }
             if constexpr (LDPC_FAST_EXP != 3) __syncthreads();
         }
@@ -340,7 +345,8 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                 for (int r = 0; r < RPT; ++r) {   // padding edges read the +inf sentinel: parity 0
                     int par = 0;
 #pragma unroll
-                    for (int k = 0; k < DC; ++k) par ^= (app[u16_at<DC>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
+                    for (int k = 0; k < DC; ++k)
+                        par ^= (app[LDPC_CHK(u16_at<DC>(colw[r], k), N + 2, CHK_FAST_GATHER)].v[c] > F(0)) ? 0 : 1;
                     synd |= par;
                 }
             }
@@ -372,6 +378,8 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
         for (int q = 0; q < 6; ++q) atomicAdd(&a.counts[q], acc[q]);
     }
 }
+
+LDPC_CHECK_TU(rows_fast)
 
 // alpha = P * 2^E with odd P < 2^20, in the range where 1/alpha is normal:
 // Markstein's correction is then exact (header).

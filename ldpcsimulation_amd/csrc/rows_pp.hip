@@ -367,6 +367,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
     constexpr bool F64 = sizeof(F) == 8;
     const F kMax = F64 ? (F)kFast64Max : (F)1e30f;   // premise bound on |yq|
     const int tid = threadIdx.x, N = g.N, lane = tid & 63;
+    [[maybe_unused]] const int EA = rs.e_pad + 64;   // c2v slots per codeword slot (LDPC_CHECK bounds)
     // check rows: schedule, and the c2v each sent last iteration, per slot
     // (entries past a row's DC are never touched, so they take no registers)
     [[maybe_unused]] int deg[RR];
@@ -407,7 +408,10 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
         for (int i = 0; i < CPT; ++i) {
             const int dg = (int)((rs.vn_info[bt * CPT + i] >> 16) & 0xffu);
             const int base = vgb[i] + lane, gd = vgd[i];
-            for (int k = dg; k < gd; ++k) s.c2v[0][base + k * 64] = s.c2v[1][base + k * 64] = z;
+            for (int k = dg; k < gd; ++k) {
+                const int e = LDPC_CHK(base + k * 64, EA, CHK_PP_BIT_READ);
+                s.c2v[0][e] = s.c2v[1][e] = z;
+            }
         }
     }
     auto vdst = [&](int i) -> int { return (int)((vdst2[i / 2] >> (16 * (i & 1))) & 0xffffu); };
@@ -449,7 +453,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                 bool in_ok = true;
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) {
-                    const P st = s.app[X][vdst(i) <= N ? vdst(i) : 0];
+                    const P st = s.app[X][LDPC_CHK(vdst(i) <= N ? vdst(i) : 0, N + 3, CHK_PP_APP_WRITE)];
 #pragma unroll
                     for (int c = 0; c < C; ++c) {
                         // yq + 0 maps -0 to +0, so app is never -0 (the fast check nodes' premise)
@@ -458,7 +462,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < CPT; ++i) s.app[X][vdst(i)] = yq[X][i];   // v2c = yq on the first pass (:364-370)
+                for (int i = 0; i < CPT; ++i) s.app[X][LDPC_CHK(vdst(i), N + 3, CHK_PP_APP_WRITE)] = yq[X][i];   // v2c = yq on the first pass (:364-370)
                 if (!in_ok) s.red[X] = 1;
             }
             P inf, zero;
@@ -505,7 +509,8 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                     constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
                     int par = 0;
 #pragma unroll
-                    for (int k = 0; k < DCr; ++k) par ^= (s.app[X][u16_at<DCX>(colw[r], k)].v[c] > F(0)) ? 0 : 1;
+                    for (int k = 0; k < DCr; ++k)
+                        par ^= (s.app[X][LDPC_CHK(u16_at<DCX>(colw[r], k), N + 3, CHK_PP_GATHER)].v[c] > F(0)) ? 0 : 1;
                     synd |= deg[r] > 0 ? par : 0;
                 });
             }
@@ -529,7 +534,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
 #pragma unroll
                         for (int k = 0; k < DCr; ++k)
                             xin[r][k] = lds_at<P>((LDPC_PP_EXP == 5 || LDPC_PP_EXP == 7) ? ab + 8u * (uint32_t)(lane + 64 * (k + 8 * r))
-                                                                                         : addr8<DCX>(colw[r], k, ab));
+                                                                                         : LDPC_ADDR8(DCX, colw[r], k, ab, N + 3, CHK_PP_GATHER));
                     });
                     if constexpr (LDPC_PP_GATHER_FIRST && LDPC_PP_PREFETCH) {
                         // every gather of the interval issued ahead of the check-node arithmetic
@@ -549,9 +554,9 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                     for (int i = 0; i < CPT; ++i) sum[i] = yq[Y][i];
                     int k = 0;
                     const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-                    vn_phases<F, C, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum);
+                    vn_phases<F, C, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum, LDPC_CHK_LIM(EA - ln), CHK_PP_BIT_READ);
 #pragma unroll
-                    for (int i = 0; i < CPT; ++i) s.app[Y][vdst(i)] = sum[i];
+                    for (int i = 0; i < CPT; ++i) s.app[Y][LDPC_CHK(vdst(i), N + 3, CHK_PP_APP_WRITE)] = sum[i];
                     if (TF && last) decide(Y, sum, wdec);   // slot Y's final pass
                 }
             }
@@ -562,7 +567,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                         constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
                         if (!LDPC_PP_PREFETCH && r > 0) {
 #pragma unroll
-                            for (int k = 0; k < DCr; ++k) xin[r][k] = lds_at<P>(addr8<DCX>(colw[r], k, ab));
+                            for (int k = 0; k < DCr; ++k) xin[r][k] = lds_at<P>(LDPC_ADDR8(DCX, colw[r], k, ab, N + 3, CHK_PP_GATHER));
                         }
                         bool ok = true;
                         // the scatter of edge k into the bit-slot layout (experiments: none, or lane-contiguous)
@@ -570,7 +575,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                             if constexpr (LDPC_PP_EXP != 4)
                                 lds_put<P>((LDPC_PP_EXP == 6 || LDPC_PP_EXP == 7)
                                                ? cb + 8u * (uint32_t)(lane + 64 * ((k + 8 * r + 16 * (tid >> 6)) % 112))
-                                               : addr8<DCX>(posw[r], k, cb),
+                                               : LDPC_ADDR8(DCX, posw[r], k, cb, EA, CHK_PP_SCATTER),
                                            m);
                         };
                         if constexpr (LDPC_PP_EXP == 3) {
@@ -631,7 +636,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                 for (int X = 0; X < 2; ++X) {
                     P post[CPT];
 #pragma unroll
-                    for (int i = 0; i < CPT; ++i) post[i] = s.app[X][vdst(i) <= N ? vdst(i) : 0];
+                    for (int i = 0; i < CPT; ++i) post[i] = s.app[X][LDPC_CHK(vdst(i) <= N ? vdst(i) : 0, N + 3, CHK_PP_APP_WRITE)];
                     decide(X, post, wdec);
                 }
             }
@@ -653,6 +658,8 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
 }
 
 }  // namespace
+
+LDPC_CHECK_TU(rows_pp)
 
 // Experiments: s_nop instructions at the kernel entry shift the code that follows by 4 bytes
 // each (the code-layout sensitivity of the loops, with and without -falign-loops).

@@ -19,7 +19,7 @@ LDPC_OK = 0
 MS, NMS, OMS, BP = 0, 1, 2, 3
 F32, F64 = 0, 1
 FLOODING, LAYERED = 0, 1
-ABI_VERSION = 10
+ABI_VERSION = 11
 # Kernel-selection options (include/ldpc_hip.h ldpc_option): tests and A/B runs set
 # them per context through the ABI; the library never reads the environment.
 OPTIONS = {"rows64": 1, "rows32": 2, "pp_slots": 3, "kernel": 4, "flood_mode": 5, "flood_msg": 6,
@@ -195,6 +195,8 @@ def lib():
     sig = {
         "ldpc_abi_version": ([], i32),
         "ldpc_f64_nms_fast_division": ([dbl], i32),
+        "ldpc_bp_math_probe": ([i32, vp, i32, vp, vp], i32),
+        "ldpc_check_selftest": ([i32], i32),
         "ldpc_last_error": ([], C.c_char_p),
         "ldpc_graph_create": ([i32, i32, vp, vp, vp, vp, C.POINTER(vp)], i32),
         "ldpc_graph_load_alist": ([C.c_char_p, C.POINTER(vp)], i32),
@@ -255,7 +257,7 @@ def lib():
 
 
 # Every symbol include/ldpc_hip.h declares (checked by tests/test_abi.py).
-EXPORTED = ["ldpc_abi_version", "ldpc_f64_nms_fast_division", "ldpc_last_error", "ldpc_graph_create", "ldpc_graph_load_alist",
+EXPORTED = ["ldpc_abi_version", "ldpc_f64_nms_fast_division", "ldpc_bp_math_probe", "ldpc_check_selftest", "ldpc_last_error", "ldpc_graph_create", "ldpc_graph_load_alist",
             "ldpc_graph_info", "ldpc_graph_destroy", "ldpc_graph_layers", "ldpc_device_count", "ldpc_ctx_create",
             "ldpc_ctx_set_stream", "ldpc_ctx_synchronize", "ldpc_ctx_destroy", "ldpc_decode_batch",
             "ldpc_sim_set_codewords", "ldpc_sim_launch", "ldpc_ctx_read_counts", "ldpc_ctx_read_histogram",

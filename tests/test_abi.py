@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     L = native.lib()
-    assert L.ldpc_abi_version() == native.ABI_VERSION == 10
+    assert L.ldpc_abi_version() == native.ABI_VERSION == 11
     with pytest.raises(native.LdpcError) as e:
         native.Graph.from_alist("/nonexistent/file.alist")
     assert e.value.code == -5

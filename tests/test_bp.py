@@ -200,3 +200,47 @@ def test_bp_rows_kernel_equals_generic_kernel(gpu_ctx_factory, monkeypatch, code
         assert int((d != d2).sum()) == 0, e
         assert cnt.as_dict() == cnt2.as_dict()
     assert got[0][3].frame_err > 0   # failing frames are compared too
+
+
+BP_TANH_ULP_TOL = 3     # device tanh (bp_math.h) vs glibc, max ulps over the check node's domain
+BP_LOG_ULP_TOL = 1      # device log vs glibc
+
+
+def _ulps(got, want):
+    got, want = np.asarray(got), np.asarray(want)
+    both_inf = np.isinf(got) & np.isinf(want) & (np.sign(got) == np.sign(want))
+    same = (got == want) | both_inf | (np.isnan(got) & np.isnan(want))
+    sp = np.spacing(np.abs(np.where(np.isfinite(want), want, 0.0)))
+    u = np.where(same, 0.0, np.abs(got - want) / np.where(sp > 0, sp, np.inf))
+    return np.where(np.isfinite(u) | same, u, np.inf)
+
+
+@pytest.mark.gpu
+def test_bp_f64_math_within_ulps_of_glibc():
+    """The fp64 BP check node's tanh and log (bp_math.h, branch-free, on the device through
+    ldpc_bp_math_probe) against glibc's (math.tanh / math.log: decodeBP.cpp:353-377 calls
+    them), over the arguments the check node forms -- v2c/2 in [-10, 10] (|v2c| <= MAXLLR
+    = 20), tiny and huge magnitudes, (1+p)/(1-p) for p in (-1, 1) -- and the specials.
+    Tolerances: BP_TANH_ULP_TOL and BP_LOG_ULP_TOL ulps."""
+    import ctypes as C
+    native = _native()
+    L = native.lib()
+    rng = np.random.default_rng(2026)
+    xt = np.concatenate([rng.uniform(-10, 10, 300000), rng.uniform(-1e-3, 1e-3, 30000),
+                         np.sign(rng.uniform(-1, 1, 30000)) * 10.0 ** rng.uniform(-310, 2.5, 30000),
+                         [0.0, -0.0, 5e-324, -5e-324, 19.0, 20.0, 25.0, -25.0, 1e300, np.inf, -np.inf, np.nan]])
+    p = np.concatenate([rng.uniform(-1, 1, 300000), 1 - 10.0 ** rng.uniform(-16, 0, 30000),
+                        -1 + 10.0 ** rng.uniform(-16, 0, 30000), rng.uniform(-1e-6, 1e-6, 30000)])
+    with np.errstate(divide="ignore"):
+        xl = np.concatenate([(1 + p) / (1 - p), 10.0 ** rng.uniform(-320, 308, 30000),
+                             [0.0, 5e-324, 1.0, np.nextafter(1.0, 2), np.nextafter(1.0, 0), np.inf, np.nan]])
+    for x, fn, tol, name in ((xt, math.tanh, BP_TANH_ULP_TOL, "tanh"), (xl, math.log, BP_LOG_ULP_TOL, "log")):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.empty_like(x)
+        args = (out.ctypes.data, None) if name == "tanh" else (None, out.ctypes.data)
+        assert L.ldpc_bp_math_probe(0, x.ctypes.data, len(x), *args) == 0, native.lib().ldpc_last_error()
+        want = np.array([fn(v) if not (name == "log" and v == 0) else -math.inf for v in x.tolist()])
+        u = _ulps(out, want)
+        hist = {k: int((u == k).sum()) for k in range(0, tol + 1)}
+        print(f"{name}: max {u.max()} ulp over {len(x)} values; histogram {hist}")
+        assert u.max() <= tol, (name, x[np.argmax(u)], out[np.argmax(u)], want[np.argmax(u)])
