@@ -92,6 +92,16 @@ PMC_PASSES = [
 ]
 
 
+# --latency: the memory pipeline's occupancy and latencies (Little's law per CU)
+LATENCY_PASSES = [
+    "TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_WRITE_REQ_sum TCP_PENDING_STALL_CYCLES_sum "
+    "GRBM_GUI_ACTIVE",
+    "TCC_REQ_sum TCC_BUSY_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum GRBM_GUI_ACTIVE",
+    "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES "
+    "TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE",
+]
+
+
 class Workload:
     """One config's context and launch, through the C ABI (native.py)."""
 
@@ -192,9 +202,9 @@ def read_pmc(d):
     return tot
 
 
-def pmc(name, lib, outdir):
+def pmc(name, lib, outdir, passes=None):
     tot = {}
-    for i, cs in enumerate(PMC_PASSES):
+    for i, cs in enumerate(passes or PMC_PASSES):
         d = os.path.join(outdir, name, f"p{i + 1}")
         shutil.rmtree(d, ignore_errors=True)
         cmd = ["rocprofv3", "--pmc"] + cs.split() + ["-d", d, "-o", "pmc", "--output-format", "csv", "--",
@@ -254,6 +264,42 @@ def fractions(line, c):
     return f
 
 
+def latency(line, c):
+    """Little's law per CU from the latency passes: average TCP->TCC read requests in
+    flight = sum of their latencies / kernel cycles; bytes per cycle = in flight x 64 B /
+    latency (the measured rate, restated); and the occupancy of the units in between."""
+    g = c.get("GRBM_GUI_ACTIVE_passes")
+    cyc = (sum(g) / len(g) / 8) if g else line["kernel_ms_best"] / 1e3 * CLOCK   # per-XCD cycles of the launch
+    out = {"kernel_cycles": cyc}
+    rq, lat = c.get("TCP_TCC_READ_REQ_sum"), c.get("TCP_TCC_READ_REQ_LATENCY_sum")
+    if rq and lat:
+        out["tcp_tcc_read_latency_cycles"] = lat / rq
+        out["tcp_tcc_reads_in_flight_per_cu"] = lat / (CUS * cyc)
+        out["tcp_tcc_read_req_per_cu_cycle"] = rq / (CUS * cyc)
+        out["littles_law_read_bytes_per_cu_cycle_64B"] = out["tcp_tcc_reads_in_flight_per_cu"] * 64 / out[
+            "tcp_tcc_read_latency_cycles"]
+    if c.get("TCP_TCC_WRITE_REQ_sum"):
+        out["tcp_tcc_write_req_per_cu_cycle"] = c["TCP_TCC_WRITE_REQ_sum"] / (CUS * cyc)
+    if c.get("TCP_PENDING_STALL_CYCLES_sum") is not None:
+        out["tcp_pending_stall_share"] = c["TCP_PENDING_STALL_CYCLES_sum"] / (CUS * cyc)
+    if c.get("TCC_EA0_RDREQ_sum") and c.get("TCC_EA0_RDREQ_LEVEL_sum"):
+        out["fabric_read_latency_cycles"] = c["TCC_EA0_RDREQ_LEVEL_sum"] / c["TCC_EA0_RDREQ_sum"]
+        out["fabric_reads_in_flight_per_xcd"] = c["TCC_EA0_RDREQ_LEVEL_sum"] / (8 * cyc)
+    if c.get("TCC_BUSY_sum"):
+        out["tcc_busy_share"] = c["TCC_BUSY_sum"] / (128 * cyc)   # 16 channels x 8 XCDs
+    if c.get("TCC_REQ_sum"):
+        out["tcc_req_per_channel_cycle"] = c["TCC_REQ_sum"] / (128 * cyc)
+    if c.get("TA_BUSY_sum"):
+        out["ta_busy_share"] = c["TA_BUSY_sum"] / (CUS * cyc)
+        out["ta_addr_stalled_by_tc_share"] = c.get("TA_ADDR_STALLED_BY_TC_CYCLES_sum", 0) / (CUS * cyc)
+    if c.get("SQ_INSTS_VMEM_RD"):
+        out["vmem_rd_instr_per_cu_cycle"] = c["SQ_INSTS_VMEM_RD"] / (CUS * cyc)
+        out["vmem_wr_instr_per_cu_cycle"] = c.get("SQ_INSTS_VMEM_WR", 0) / (CUS * cyc)
+    if c.get("SQ_WAIT_ANY") and c.get("SQ_WAVE_CYCLES"):
+        out["wait_any_share"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+    return out
+
+
 def roofline(line, f):
     """The binding resource: the largest fraction (LDS kernels keep the algorithmic model)."""
     cand = {k: v for k, v in f.items() if k in ("lds", "valu", "hbm")}
@@ -279,6 +325,7 @@ def main():
     ap.add_argument("--out", default=None, help="append the JSON lines here too")
     ap.add_argument("--child", default=None)
     ap.add_argument("--lib", default=None, help="A/B only: another build of the decoder library")
+    ap.add_argument("--latency", action="store_true", help="also the memory-latency passes (Little's law)")
     a = ap.parse_args()
     if a.child:
         child(a.child, a.lib)
@@ -305,6 +352,10 @@ def main():
             line["pmc"] = {k: v for k, v in c.items()}
             line["pmc_source"] = "rocprofv3 --pmc, %d passes over one launch (%s)" % (
                 len(PMC_PASSES), os.path.relpath(os.path.join(a.pmc_dir, n), ROOT))
+        if a.latency:
+            cl = pmc(n, a.lib, os.path.join(a.pmc_dir, "latency"), LATENCY_PASSES)
+            line["latency"] = latency(line, cl)
+            line["latency_pmc"] = cl
         s = json.dumps(line)
         print(s, flush=True)
         if a.out:
