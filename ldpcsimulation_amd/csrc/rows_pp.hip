@@ -145,10 +145,9 @@ namespace {
 constexpr int kPPRole = 512;          // threads per role
 constexpr int kPPWaves = 2 * kPPRole / 64;
 constexpr int kPPMaxCw = 4;           // codewords per block step (2 slots x an fp32 pair)
-// red[] ints: [0,2) slot flags, [32, 32 + 3 x 4 codewords) the block totals (pp_account's LDS
-// atomics), then acc (6 x u64); the pipelined fp64 kernel's staging area follows red[]
+// red[] ints: [0,2) slot flags, [32, 32 + 16 waves x 3 x 4 codewords) block sums, then acc (6 x u64)
 constexpr int kPPRedSums = 32;
-constexpr int kPPRedAcc = kPPRedSums + 3 * kPPMaxCw;
+constexpr int kPPRedAcc = kPPRedSums + kPPWaves * 3 * kPPMaxCw;
 constexpr int kPPRedInts = kPPRedAcc + 2 * 6 + 4;
 static_assert(kPPRedAcc % 2 == 0 && kPPRedAcc + 2 * 6 <= kPPRedInts, "acc (6 x u64) outside red[]");
 
@@ -658,331 +657,6 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
     PP_STAMP_OUT()
 }
 
-// ---- fp64: the per-step work inside the barrier intervals (LDPC_PP_PIPE, round 6) ----
-// pp_role ends each step with work done between barriers by one role while the other
-// waits -- the channel of both codewords, their staging, the syndrome, the decisions and
-// the block reduction (7.5 intervals' worth of time per step, 0.95 ms of the 12.3 ms
-// launch: the intercept of kernel time against T). Here each slot's codeword ends and the
-// next begins inside intervals that also carry the other role's work. One step, 2T + 3
-// intervals:
-//   i = 0        | c_0(0)                         | yq(1)                             |
-//   i = 2t+1     | c_t(1)                         | b_t(0)   (+ decide(0) at t = T-1) |
-//   i = 2t+2     | c_{t+1}(0); syndrome(0) at T-1 | b_t(1)   (+ decide(1) at t = T-1) |
-//   i = 2T+1     | syndrome(1), account(0)        | channel(0) of the next step       |
-//   i = 2T+2     | account(1)                     | yq(0), channel(1) of the next step|
-// channel(X): Philox4x32-10 + the fp32 Box-Muller normals of slot X's next codeword into
-// the staging area S[X] (the fp64 channel widens the fp32 normals, so staging them is
-// exact; 2 x N floats after red[]). yq(X): the owner of each bit slot forms
-// y = c (1 + sigma n) (or reads the given y), the front end, yq + 0, its uncoded error
-// and the premise test, into app[X] -- the values pp_channel + the staging of pp_role
-// produce. Every hand-over crosses a barrier: app[X] final after b_{T-1}(X) ->
-// syndrome(X) -> yq(X) of the next codeword -> c_0(X); S[X]: channel(X) -> yq(X); red[X]
-// and the totals tot[3X .. 3X+2] are read and cleared by thread 0 (account) in the
-// interval after their codeword's last writer and written for the next codeword only
-// after that. The arithmetic of every check and bit node is pp_role's.
-template <int SRC, int DC0, int DC1, int CPT, int VAR, bool FDIV, int R, bool HB>
-__device__ __forceinline__ void pp_role_pipe(const DecodeArgs &a, const DevGraph &g, const RowSched &rs,
-                                             const PPSlots<Pack<double, 1>> &s, float *stage, unsigned *redo,
-                                             unsigned long long *acc)
-{
-    using F = double;
-    using P = Pack<double, 1>;
-    constexpr int DCX = 8;
-    constexpr int RR = R > 0 ? R : 1;
-    static_assert(DC0 <= DCX && DC1 <= DCX && (R == 0) == HB, "pp_role_pipe shape");
-    static_assert(!LDPC_BM64, "the staged normals are the fp32 Box-Muller's");
-    const F kMax = (F)kFast64Max;
-    const int tid = threadIdx.x, N = g.N, lane = tid & 63;
-    [[maybe_unused]] const int EA = rs.e_pad + 64;
-    [[maybe_unused]] int deg[RR];
-    [[maybe_unused]] uint32_t colw[RR][DCX / 2], posw[RR][DCX / 2];
-    [[maybe_unused]] P prev[2][RR][DCX];
-    if constexpr (R > 0) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int j = tid + r * kPPRole;
-            deg[r] = rs.cn_deg[j];
-            const uint4 xc = reinterpret_cast<const uint4 *>(rs.cn_cols + (size_t)j * DCX)[0];
-            const uint4 xp = reinterpret_cast<const uint4 *>(rs.cn_pos + (size_t)j * DCX)[0];
-            colw[r][0] = xc.x; colw[r][1] = xc.y; colw[r][2] = xc.z; colw[r][3] = xc.w;
-            posw[r][0] = xp.x; posw[r][1] = xp.y; posw[r][2] = xp.z; posw[r][3] = xp.w;
-            if (deg[r] == 0)   // rows past M: gather the +0 entry, so their messages stay 0
-#pragma unroll
-                for (int q = 0; q < DCX / 2; ++q) colw[r][q] = (uint32_t)(N + 2) * 0x10001u;
-        }
-    }
-    const int bt = tid - kPPRole;
-    [[maybe_unused]] int vgb[CPT], vgd[CPT];
-    [[maybe_unused]] uint32_t vdst2[(CPT + 1) / 2] = {};
-    if constexpr (HB) {
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int c = rs.vn_col[bt * CPT + i];
-            vdst2[i / 2] |= (uint32_t)(c == 0xffff ? N + 1 : c) << (16 * (i & 1));
-            const uint32_t info = rs.vn_info[bt * CPT + i];
-            vgb[i] = __builtin_amdgcn_readfirstlane((int)(info & 0xffffu) - lane);
-            vgd[i] = __builtin_amdgcn_readfirstlane((int)(info >> 24));
-        }
-        P z;
-        z.v[0] = F(0);
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {   // padding slots of the bit-node layout hold +0; never written
-            const int dg = (int)((rs.vn_info[bt * CPT + i] >> 16) & 0xffu);
-            const int base = vgb[i] + lane, gd = vgd[i];
-            for (int k = dg; k < gd; ++k) {
-                const int e = LDPC_CHK(base + k * 64, EA, CHK_PP_BIT_READ);
-                s.c2v[0][e] = s.c2v[1][e] = z;
-            }
-        }
-    }
-    auto vdst = [&](int i) -> int { return (int)((vdst2[i / 2] >> (16 * (i & 1))) & 0xffffu); };
-    const F alpha = (F)a.alpha, delta = (F)a.delta, rcp = (F)(1.0 / a.alpha);
-    const int nsteps = (a.batch + 1) / 2;
-    int *tot = s.red + kPPRedSums;
-    const bool lane0 = lane == 0;
-    [[maybe_unused]] P yq[2][CPT];
-    [[maybe_unused]] int unc[2] = {0, 0}, wdec[2] = {0, 0};
-    if constexpr (R > 0) {
-#pragma unroll
-        for (int X = 0; X < 2; ++X)
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int k = 0; k < DCX; ++k) prev[X][r][k].v[0] = F(0);
-    }
-    auto cw_vec = [&](int b) -> const int8_t * {
-        return SRC == SRC_GIVEN ? (a.c ? a.c + (size_t)b * N : nullptr)
-                                : (a.cw_table ? a.cw_table + (size_t)((a.first_cw + (uint64_t)b) % (uint64_t)a.cw_rows) * N
-                                              : nullptr);
-    };
-    // channel(X, grp): the normals of codeword 2 grp + X into S[X] (bit role, one Philox group per thread)
-    auto channel = [&](int X, int grp) {
-        if constexpr (SRC != SRC_GIVEN) {
-            const int b = grp * 2 + X;
-            if (b >= a.batch) return;
-            const uint64_t cw = a.first_cw + (uint64_t)b;
-            float *S = stage + X * N;
-            const int ng4 = (N + 3) / 4;
-            for (int g4 = bt; g4 < ng4; g4 += kPPRole) {
-                uint32_t u[4];
-                philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, (uint32_t)a.seed,
-                                    (uint32_t)(a.seed >> 32), u);
-                float n[4];
-                box_muller(u[0], u[1], n[0], n[1]);
-                box_muller(u[2], u[3], n[2], n[3]);
-#pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4)
-                    if (4 * g4 + q4 < N) S[4 * g4 + q4] = n[q4];
-            }
-        }
-    };
-    // yq(X, grp): each bit slot's channel value (:214-238), front end, yq + 0 (so app is
-    // never -0), uncoded error and premise, into app[X] and yq[X] (bit role)
-    auto load_yq = [&](auto Xc, int grp) {
-        constexpr int X = decltype(Xc)::value;
-        const int b = grp * 2 + X;
-        const bool have = b < a.batch;   // a missing codeword: +1 samples, never counted
-        const int8_t *cvec = have ? cw_vec(b) : nullptr;
-        const float *S = stage + X * N;
-        const F sigma = (F)a.sigma;
-        bool in_ok = true;
-        int e = 0;
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int v = vdst(i);
-            F q = F(0);
-            if (v < N) {
-                const int cv = cvec ? cvec[v] : 1;
-                F yv = F(1);
-                if (have) {
-                    if (SRC == SRC_GIVEN) {
-                        yv = reinterpret_cast<const F *>(a.y)[(size_t)b * N + v];
-                    } else {
-                        yv = (F)cv * (F(1) + sigma * (F)S[v]);
-                        if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
-                    }
-                }
-                q = front_end<F>(yv, a);
-                e += ((q > F(0) ? 1 : -1) * cv < 0);
-            }
-            yq[X][i].v[0] = q + F(0);
-            in_ok &= dabs(yq[X][i].v[0]) < kMax;
-            s.app[X][LDPC_CHK(vdst(i), N + 3, CHK_PP_APP_WRITE)] = yq[X][i];   // v2c = yq on the first pass (:364-370)
-        }
-        unc[X] = have ? e : 0;
-        if (!in_ok) s.red[X] = 1;
-    };
-    // the check rows of slot X (pp_role's interval, product settings)
-    auto rows = [&](auto Xc) {
-        constexpr int X = decltype(Xc)::value;
-        if constexpr (R > 0) {
-            P xin[RR][DCX];
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int q = 0; q < DCX / 2; ++q) asm volatile("" : "+v"(colw[r][q]), "+v"(posw[r][q]));
-            const uint32_t ab = s.app_base[X], cb = s.c2v_base[X];
-            static_for<0, R>([&](auto rc) {
-                constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
-#pragma unroll
-                for (int k = 0; k < DCr; ++k) xin[r][k] = lds_at<P>(LDPC_ADDR8(DCX, colw[r], k, ab, N + 3, CHK_PP_GATHER));
-            });
-            static_for<0, R>([&](auto rc) {
-                constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
-                auto store = [&](int k, const P &m) { lds_put<P>(LDPC_ADDR8(DCX, posw[r], k, cb, EA, CHK_PP_SCATTER), m); };
-                uint32_t pa = 0;
-                pp_check_node<F, DCr, VAR, FDIV>(xin[r], prev[X][r], alpha, rcp, delta, store, &pa);
-                if (__builtin_amdgcn_ballot_w64(pa >= kFast64MaxHi)) {   // rare: M2 >= 2^1000 or a tiny minimum
-                    asm volatile(";");   // a side effect: stays a skipped branch
-                    if (pa >= kFast64MaxHi) s.red[X] = 1;
-                }
-                if (R > 1) __builtin_amdgcn_sched_barrier(0);   // keep the rows' live ranges apart
-            });
-        }
-    };
-    // the bit nodes of slot Y (:452-476); at its codeword's last pass also the decisions, error
-    // weight (:270, :382-393) and the wave sums of the weight and the uncoded errors into tot
-    auto bits = [&](auto Yc, auto lastc, int grp) {
-        constexpr int Y = decltype(Yc)::value;
-        constexpr bool last = decltype(lastc)::value;
-        if constexpr (HB) {
-#pragma unroll
-            for (int q = 0; q < (CPT + 1) / 2; ++q) asm volatile("" : "+v"(vdst2[q]));
-            P sum[CPT];
-#pragma unroll
-            for (int i = 0; i < CPT; ++i) sum[i] = yq[Y][i];
-            int k = 0;
-            const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-            vn_phases<F, 1, CPT, CPT>(s.c2v[Y] + ln, vgb, vgd, k, sum, LDPC_CHK_LIM(EA - ln), CHK_PP_BIT_READ);
-#pragma unroll
-            for (int i = 0; i < CPT; ++i) s.app[Y][LDPC_CHK(vdst(i), N + 3, CHK_PP_APP_WRITE)] = sum[i];
-            if constexpr (last) {
-                const int b = grp * 2 + Y;
-                int e = 0;
-                if (b < a.batch) {
-                    const int8_t *cvec = cw_vec(b);
-#pragma unroll
-                    for (int i = 0; i < CPT; ++i) {
-                        const int v = vdst(i);
-                        if (v < N) {
-                            const int d = sum[i].v[0] > F(0) ? 1 : -1;   // :471-474
-                            const int cv = cvec ? cvec[v] : 1;
-                            e += (d != cv);
-                            if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
-                        }
-                    }
-                }
-                const int w = wave_sum3(e), u = wave_sum3(unc[Y]);
-                if (lane0 && w) atomicAdd(&tot[3 * Y], w);
-                if (lane0 && u) atomicAdd(&tot[3 * Y + 1], u);
-            }
-        }
-    };
-    // the syndrome of slot X's codeword (rows; padding edges read +inf: parity 0) into tot
-    auto syndrome = [&](int X) {
-        if constexpr (R > 0) {
-            int synd = 0;
-            static_for<0, R>([&](auto rc) {
-                constexpr int r = decltype(rc)::value, DCr = r == 0 ? DC0 : DC1;
-                int par = 0;
-#pragma unroll
-                for (int k = 0; k < DCr; ++k)
-                    par ^= (s.app[X][LDPC_CHK(u16_at<DCX>(colw[r], k), N + 3, CHK_PP_GATHER)].v[0] > F(0)) ? 0 : 1;
-                synd |= deg[r] > 0 ? par : 0;
-            });
-            if (__builtin_amdgcn_ballot_w64(synd != 0) && lane0) atomicAdd(&tot[3 * X + 2], 1);
-        }
-    };
-    // thread 0: slot X's codeword of step grp into the block totals, or onto the re-decode list
-    auto account = [&](int X, int grp) {
-        if (tid != 0) return;
-        const int fl = s.red[X];
-        s.red[X] = 0;
-        const int w = tot[3 * X], uc = tot[3 * X + 1], sf = tot[3 * X + 2] > 0;
-        tot[3 * X] = tot[3 * X + 1] = tot[3 * X + 2] = 0;
-        const int b = grp * 2 + X;
-        if (b >= a.batch) return;
-        if (fl) {
-            const unsigned at = atomicAdd(&redo[0], 1u);
-            redo[1 + at] = (unsigned)b;
-            return;
-        }
-        acc[0] += (unsigned long long)w;
-        acc[1] += (unsigned long long)(w > 0);
-        acc[2] += (unsigned long long)uc;
-        acc[3] += 1ull;
-        acc[5] += (unsigned long long)sf;
-        if (w > 0 && a.hist) atomicAdd(&a.hist[w - 1], 1ull);
-        if (a.frame_res) a.frame_res[b] = make_int4(w, uc, sf, 0);
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using Last = std::true_type;
-    using NotLast = std::false_type;
-    PP_STAMP_DECL;
-    int grp = blockIdx.x;
-    if (grp < nsteps) {
-        // prologue: the first step's channel and slot 0's staging
-        if constexpr (HB) {
-            P inf, zero;
-            inf.v[0] = dinf<F>();
-            zero.v[0] = F(0);
-            if (tid == kPPRole) s.app[0][N] = s.app[1][N] = inf;
-            if (tid == kPPRole + 1) s.app[0][N + 2] = s.app[1][N + 2] = zero;
-            channel(0, grp);
-            channel(1, grp);
-        }
-        PP_BARRIER();
-        if constexpr (HB) load_yq(I0(), grp);
-        PP_BARRIER();
-    }
-    for (; grp < nsteps; grp += gridDim.x) {
-        const int nxt = grp + (int)gridDim.x;
-        rows(I0());                       // i = 0: c_0(0) | yq(1)
-        if constexpr (HB) load_yq(I1(), grp);
-        PP_BARRIER();
-        for (int t = 0; t + 1 < a.T; ++t) {
-            rows(I1());                   // i = 2t+1: c_t(1) | b_t(0)
-            bits(I0(), NotLast(), grp);
-            PP_BARRIER();
-            rows(I0());                   // i = 2t+2: c_{t+1}(0) | b_t(1)
-            bits(I1(), NotLast(), grp);
-            PP_BARRIER();
-        }
-        rows(I1());                       // i = 2T-1: c_{T-1}(1) | b_{T-1}(0), decide(0)
-        bits(I0(), Last(), grp);
-        PP_BARRIER();
-        syndrome(0);                      // i = 2T: syndrome(0) | b_{T-1}(1), decide(1)
-        bits(I1(), Last(), grp);
-        PP_BARRIER();
-        // i = 2T+1: syndrome(1), slot 0 accounted, the old messages cleared | channel(0) of the next step
-        syndrome(1);
-        account(0, grp);
-        if constexpr (R > 0) {
-#pragma unroll
-            for (int X = 0; X < 2; ++X)
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-#pragma unroll
-                    for (int k = 0; k < DCX; ++k) prev[X][r][k].v[0] = F(0);
-        }
-        if constexpr (HB) {
-            if (nxt < nsteps) channel(0, nxt);
-        }
-        PP_BARRIER();
-        // i = 2T+2: slot 1 accounted | yq(0) and channel(1) of the next step
-        account(1, grp);
-        if constexpr (HB) {
-            if (nxt < nsteps) {
-                load_yq(I0(), nxt);
-                channel(1, nxt);
-            }
-        }
-        PP_BARRIER();
-    }
-    PP_STAMP_OUT()
-}
-
 }  // namespace
 
 LDPC_CHECK_TU(rows_pp)
@@ -996,7 +670,7 @@ LDPC_CHECK_TU(rows_pp)
 // SPLIT: the schedule has degree-aware row slots (rs.dc_low == 7, graph.h
 // pp_row_slots): check waves 4-7 run two 7-edge rows, waves 0-3 a 7-edge and an
 // 8-edge row. Otherwise every row runs the 8-edge check node.
-template <typename F, int SRC, int CPT, int VAR, bool FDIV, bool SPLIT, bool PIPE = false>
+template <typename F, int SRC, int CPT, int VAR, bool FDIV, bool SPLIT>
 __global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph g, RowSched rs, unsigned *redo)
 {
     using P = Pack<F, PPCw<F>::C>;
@@ -1023,27 +697,14 @@ __global__ __launch_bounds__(2 * kPPRole) void k_rows_pp(DecodeArgs a, DevGraph 
         if (wave >= kPPRole / 128) __builtin_amdgcn_s_setprio(2);
         else __builtin_amdgcn_s_setprio(1);
     }
-    if constexpr (PIPE) {
-        static_assert(sizeof(F) == 8, "the pipelined step is the fp64 kernel's");
-        float *stage = reinterpret_cast<float *>(s.red + kPPRedInts);
-        if (!low)
-            pp_role_pipe<SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, stage, redo, acc);
-        else if (!SPLIT)
-            pp_role_pipe<SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, stage, redo, acc);
-        else if (wave >= kPPRole / 128)
-            pp_role_pipe<SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, stage, redo, acc);
-        else
-            pp_role_pipe<SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, stage, redo, acc);
-    } else {
-        if (!low)
-            pp_role<F, SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
-        else if (!SPLIT)
-            pp_role<F, SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-        else if (wave >= kPPRole / 128)
-            pp_role<F, SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-        else
-            pp_role<F, SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
-    }
+    if (!low)
+        pp_role<F, SRC, 8, 8, CPT, VAR, FDIV, 0, true>(a, g, rs, s, redo, acc);
+    else if (!SPLIT)
+        pp_role<F, SRC, 8, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+    else if (wave >= kPPRole / 128)
+        pp_role<F, SRC, 7, 7, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
+    else
+        pp_role<F, SRC, 7, 8, CPT, VAR, FDIV, 2, false>(a, g, rs, s, redo, acc);
     if (threadIdx.x == 0 && acc[3] > 0) {
         acc[4] = acc[3] * (unsigned long long)a.T;
 #pragma unroll
@@ -1055,11 +716,6 @@ int rows_pp_lds_bytes(const DevGraph &g, const RowSched &rs)
 {
     return (int)(2 * (size_t)(g.N + 3 + rs.e_pad + 64) * 8 + kPPRedInts * sizeof(int));
 }
-// + the pipelined fp64 kernel's staging area: the fp32 normals of both slots' next codewords
-static int rows_pp_pipe_lds_bytes(const DevGraph &g, const RowSched &rs)
-{
-    return rows_pp_lds_bytes(g, rs) + 2 * g.N * (int)sizeof(float);
-}
 
 bool rows_pp_supported(const DevGraph &g, const RowSched &rs)
 {
@@ -1069,22 +725,12 @@ bool rows_pp_supported(const DevGraph &g, const RowSched &rs)
            g.N <= 4 * kPPRole && g.N + 3 <= 0xffff && rows_pp_lds_bytes(g, rs) <= 160 * 1024;
 }
 
-// fp64 with T >= 1 runs the pipelined step when its staging area fits (LDPC_PP_PIPE; 0: the
-// step of pp_role, as fp32 and T = 0 always do)
-#ifndef LDPC_PP_PIPE
-#define LDPC_PP_PIPE 1
-#endif
 template <typename F, int SRC, int VAR, bool FDIV>
 static hipError_t launch_pp_t(const DevGraph &g, const RowSched &rs, const DecodeArgs &a, unsigned *redo,
                               hipStream_t s, int num_cus)
 {
-    const bool pipe = LDPC_PP_PIPE && sizeof(F) == 8 && a.T > 0 && rows_pp_pipe_lds_bytes(g, rs) <= 160 * 1024;
     auto fn = rs.dc_low == 7 ? k_rows_pp<F, SRC, 4, VAR, FDIV, true> : k_rows_pp<F, SRC, 4, VAR, FDIV, false>;
-    if constexpr (sizeof(F) == 8) {
-        if (pipe)
-            fn = rs.dc_low == 7 ? k_rows_pp<F, SRC, 4, VAR, FDIV, true, true> : k_rows_pp<F, SRC, 4, VAR, FDIV, false, true>;
-    }
-    const int lds = pipe ? rows_pp_pipe_lds_bytes(g, rs) : rows_pp_lds_bytes(g, rs);
+    const int lds = rows_pp_lds_bytes(g, rs);
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     constexpr int CW = 2 * PPCw<F>::C;

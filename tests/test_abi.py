@@ -88,16 +88,13 @@ def test_shipped_library_holds_only_the_kept_ping_pong_kernel():
     import subprocess
     syms = subprocess.run(["nm", "-C", native.LIB_PATH], capture_output=True, text=True, check=True).stdout
     kern = sorted({m for m in re.findall(r"ldpc::k_rows_pp<([^>]*)>", syms)})
-    # fp64: 2 sources x (MS, OMS, NMS, NMS Markstein) x 2 row-slot layouts, each with the
-    # pipelined step (T >= 1, round 6) and pp_role's step (T = 0);
-    # fp32 pairs: 2 sources x (MS, NMS with the verified reciprocal) x 2 layouts, pp_role's step
-    assert len(kern) == 40, kern
+    # fp64: 2 sources x (MS, OMS, NMS, NMS Markstein) x 2 row-slot layouts;
+    # fp32 pairs: 2 sources x (MS, NMS with the verified reciprocal) x 2 layouts
+    assert len(kern) == 24, kern
     for k in kern:
-        ft, src, cpt, var, fdiv, split, pipe = (x.strip() for x in k.split(","))
+        ft, src, cpt, var, fdiv, split = (x.strip() for x in k.split(","))
         assert ft in ("double", "float") and cpt == "4" and split in ("true", "false") and src in ("0", "1"), k
-        assert pipe == "false" or ft == "double", k
     assert sum(k.startswith("float") for k in kern) == 8
-    assert sum(k.endswith("true") and k.startswith("double") for k in kern) == 16
     with open(native.LIB_PATH, "rb") as f:
         blob = f.read()
     assert b"LDPC_PP_MODE" not in blob and b"pp_wait" not in blob
