@@ -38,16 +38,36 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-// Uniforms in (0,1): (u + 1/2) * 2^-32.
+// Uniforms in (0,1): (u + 1/2) * 2^-32; n0, n1 = sqrt(-2 ln r) (cos, sin)(2 pi a).
+// The transform runs on the SIMD's own transcendental instructions: v_log_f32 (log2, so
+// -2 ln r = -2 ln 2 * log2 r), v_sqrt_f32, and v_sin_f32 / v_cos_f32, whose argument is in
+// revolutions (sin(2 pi a) is v_sin_f32(a), a in (0, 1)): five instructions where OCML's
+// correctly-rounded logf / sqrtf / sincospif took ~100 with their range and denormal
+// branches. r >= 2^-33 is a normal float, so the hardware log is within an ulp or two; the
+// normals differ from the OCML transform's in the last bits only, which no Gaussian
+// statistic resolves (test_channel_noise_statistics, the FER z-tests). LDPC_BM_OCML=1
+// (variant builds) keeps the OCML transform for A/B.
+#ifndef LDPC_BM_OCML
+#define LDPC_BM_OCML 0
+#endif
+#if LDPC_BM_OCML != 0 && !defined(LDPC_AB_BUILD)
+#error "LDPC_BM_OCML changes the noise the parity tests pin: variant builds only"
+#endif
 __device__ __forceinline__ void box_muller(uint32_t ua, uint32_t ur, float &n0, float &n1)
 {
     const float a = (float)ua * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
     const float r = (float)ur * 2.3283064365386963e-10f + 1.1641532182693481e-10f;
-    const float rad = sqrtf(-2.0f * logf(r));
-    float s, c;
-    sincospif(2.0f * a, &s, &c);
-    n0 = rad * c;
-    n1 = rad * s;
+    if constexpr (!LDPC_BM_OCML) {
+        const float rad = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(r));
+        n0 = rad * __builtin_amdgcn_cosf(a);
+        n1 = rad * __builtin_amdgcn_sinf(a);
+    } else {
+        const float rad = sqrtf(-2.0f * logf(r));
+        float s, c;
+        sincospif(2.0f * a, &s, &c);
+        n0 = rad * c;
+        n1 = rad * s;
+    }
 }
 // The fp64 channel's normals: the fp32 transform above, widened to double (SURVEY
 // §8 a2: Philox4x32-10 + Box-Muller in fp32). The decoders compute in fp64 on the

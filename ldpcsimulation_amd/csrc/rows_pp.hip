@@ -121,7 +121,7 @@ namespace {
 // Diagnostic builds (-DLDPC_STAMPS, `make ppvariant`): per wave, s_memtime cycles
 // spent working and waiting at the interval barriers, to a.stamps[(block*16+wave)*2].
 #ifdef LDPC_STAMPS
-#define PP_STAMP_DECL unsigned long long st_work = 0, st_wait = 0, st_t0 = __builtin_amdgcn_s_memtime()
+#define PP_STAMP_DECL unsigned long long st_work = 0, st_wait = 0, st_step[5] = {}, st_t0 = __builtin_amdgcn_s_memtime()
 #define PP_BARRIER()                                                        \
     do {                                                                    \
         const unsigned long long te_ = __builtin_amdgcn_s_memtime();        \
@@ -131,14 +131,34 @@ namespace {
         st_wait += tb_ - te_;                                               \
         st_t0 = tb_;                                                        \
     } while (0)
+// Per step, to a.stamps[8192 + (block*16+wave)*6 + k]: k = 0 the tail (last interval
+// barrier -> the next step's top: syndrome, decisions, the block accounting), 1 the channel
+// (step top -> B1), 2 the wait at B1, 3 the yq staging (B1 -> B2), 4 the wait at B2.
+#define PP_STAMP_ACC(k)                                                     \
+    do {                                                                    \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();         \
+        st_step[k] += t_ - st_t0;                                           \
+        st_t0 = t_;                                                         \
+    } while (0)
+#define PP_STAMP_TOP() PP_STAMP_ACC(0)
+#define PP_SYNC_STAMPED(k0)                                                 \
+    do {                                                                    \
+        PP_STAMP_ACC(k0);                                                   \
+        __syncthreads();                                                    \
+        PP_STAMP_ACC(k0 + 1);                                               \
+    } while (0)
 #define PP_STAMP_OUT()                                                                              \
     if (a.stamps && (threadIdx.x & 63) == 0 && blockIdx.x < 256) {                                  \
         a.stamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 2] = st_work;                             \
         a.stamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 2 + 1] = st_wait;                         \
+        for (int k_ = 0; k_ < 5; ++k_)                                                              \
+            a.stamps[8192 + (blockIdx.x * 16 + (threadIdx.x >> 6)) * 6 + k_] = st_step[k_];         \
     }
 #else
 #define PP_STAMP_DECL
 #define PP_BARRIER() __syncthreads()
+#define PP_STAMP_TOP()
+#define PP_SYNC_STAMPED(k0) __syncthreads()
 #define PP_STAMP_OUT()
 #endif
 
@@ -419,6 +439,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
     const int nsteps = (a.batch + 2 * C - 1) / (2 * C);
     PP_STAMP_DECL;
     for (int grp = blockIdx.x; grp < nsteps; grp += gridDim.x) {
+        PP_STAMP_TOP();
         [[maybe_unused]] uint32_t pacc[2] = {0u, 0u};   // fp64, LDPC_PP_STICKY: per-slot premise maximum
         constexpr bool TF = (LDPC_PP_TAILFUSE & (F64 ? 2 : 1)) != 0;
         int unc[2 * C];
@@ -435,7 +456,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
                     for (int c = 0; c < C; ++c) s.app[0][v].v[c] = s.app[1][v].v[c] = F(1);
             }
         }
-        __syncthreads();   // B1: channel staged
+        PP_SYNC_STAMPED(1);   // B1: channel staged
         [[maybe_unused]] P yq[2][CPT];
         if constexpr (R > 0) {
 #pragma unroll
@@ -474,7 +495,7 @@ __device__ __forceinline__ void pp_role(const DecodeArgs &a, const DevGraph &g, 
             if (tid == kPPRole) s.app[0][N] = s.app[1][N] = inf;
             if (tid == kPPRole + 1) s.app[0][N + 2] = s.app[1][N + 2] = zero;
         }
-        __syncthreads();   // B2: yq in app
+        PP_SYNC_STAMPED(3);   // B2: yq in app
 
         // Decisions and error weight of slot Y's codewords from its final posteriors
         // (bit slots; :270, :382-393), into w[Y*C + c].

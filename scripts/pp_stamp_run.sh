@@ -11,4 +11,4 @@ O=gpurun_out/stamps_$TAG; mkdir -p $O; rm -f $O/st.bin
 LDPC_STAMPS=$PWD/$O/st.bin timeout -k 10 300 python bench.py --lib ${STAMP_LIB:-ab/libldpc_hip_ppst.so} --no-cpu-baseline --no-secondary --steps 2 --warmup 1 --live-pmc off --precision $PREC "$@" > $O/b.json 2> $O/b.err || { tail -5 $O/b.err; exit 1; }
 # 65536 codewords / 256 blocks: 128 fp64 pairs (or 64 steps of two fp32 pairs) per block, 2T+1 = 101 intervals each
 STEPS=$([ "$PREC" = f32 ] && echo 64 || echo 128)
-python scripts/pp_stamps.py $O/st.bin $((STEPS * 101)) | tee $O/stamps.txt
+python scripts/pp_stamps.py $O/st.bin $((STEPS * 101)) $STEPS | tee $O/stamps.txt
