@@ -297,3 +297,24 @@ def test_binary_context_refuses_ems_options_and_orders_stream_changes():
     ctx.synchronize()
     ctx.set_stream(None)
     assert ctx.read_counts(reset=True).as_dict() == gref.as_dict()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec,batch", [("f64", 4096), ("f64", 1001), ("f32", 4096), ("f32", 1003)])
+def test_pp_channel_fast_step_equals_general_loop(gpu_ctx_factory, prec, batch):
+    """The channel's straight-line common step (rows_pp.hip pp_channel: all codewords of the
+    step in the batch, no codeword table, no front end, no sample output) gives the general
+    loop's values: sim_batch takes the fast step, sim_trace (which writes the samples) the
+    general loop, on the same seed -- per-frame results, counters and the re-decode list
+    identical; a ragged batch runs its last step on the general loop in both."""
+    from ldpcsimulation_amd import native
+    ctx = gpu_ctx_factory(CODE)
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=20,
+                               precision=native.F64 if prec == "f64" else native.F32)
+    assert ctx.kernel_info(cfg)["kernel"] == "rows_pp"
+    f_fast, c_fast = ctx.sim_batch(1.25, 0.5, cfg, seed=5150, stream_id=2, first_cw=999, batch=batch)
+    r_fast = ctx.redo_count()
+    y, d, f_gen, c_gen = ctx.sim_trace(1.25, 0.5, cfg, seed=5150, stream_id=2, first_cw=999, batch=batch)
+    assert np.array_equal(f_fast, f_gen)
+    assert c_fast.as_dict() == c_gen.as_dict() and r_fast == ctx.redo_count() == 0
+    assert c_gen.frame_err > 0 and c_gen.uncoded_bit_err > 0
