@@ -81,6 +81,14 @@ namespace ldpc {
 #if LDPC_FAST_EXP != 0 && !defined(LDPC_AB_BUILD)
 #error "LDPC_FAST_EXP != 0 gives wrong results by design: make fastvariant only"
 #endif
+// 1: no staging barrier per codeword group -- the channel writes yq + 0 into app itself and
+// flags the premise (raised after the channel's barrier, where thread 0 has cleared the
+// flag), each thread reads its yq back, and the bit-layout padding slots are zeroed once per
+// kernel (nothing else writes them); 0: the channel is staged through the c2v area and
+// copied to app between two barriers, the padding slots re-zeroed every group.
+#ifndef LDPC_FAST_NOB2
+#define LDPC_FAST_NOB2 1
+#endif
 template <int RPT> struct FastShape;
 #ifndef LDPC_FAST_RPT1_WAVES
 #define LDPC_FAST_RPT1_WAVES 4
@@ -151,10 +159,32 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
 #pragma unroll
         for (int q = 0; q < 3 * C; ++q) red[32 + q] = 0;   // block_sum_lds totals
     }
+    if constexpr (LDPC_FAST_NOB2) {   // padding slots of the bit-node layout hold +0 (never written)
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int dg = (int)((rs.vn_info[tid * CPT + i] >> 16) & 0xffu);
+            const int base = vgb[i] + lane, gd = vgd[i];
+            P z;
+#pragma unroll
+            for (int c = 0; c < C; ++c) z.v[c] = F(0);
+            for (int k = dg; k < gd; ++k) c2v[LDPC_CHK(base + k * 64, EA, CHK_FAST_BIT_READ)] = z;
+        }
+    }
+    // the channel's destination: app itself (LDPC_FAST_NOB2, canonical yq) or the c2v staging area
+    P *const stage = LDPC_FAST_NOB2 ? app : c2v;
     for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
-        // ---- channel (:214-238), staged through the c2v area ----
+        // ---- channel (:214-238) ----
         if (tid == 0) red[31] = 0;
         int unc[C];
+        [[maybe_unused]] bool ch_ok = true;   // LDPC_FAST_NOB2: this thread's inputs within the premise
+        // LDPC_FAST_NOB2: the staged value is yq + 0 (app never holds -0), checked against the bound
+        auto put = [&](int v, int c, F q) {
+            if constexpr (LDPC_FAST_NOB2) {
+                q = q + F(0);
+                ch_ok &= dabs(q) < kMax;
+            }
+            stage[v].v[c] = q;
+        };
         const int8_t *cvec[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
@@ -162,7 +192,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             cvec[c] = nullptr;
             const int b = grp * C + c;
             if (b >= a.batch) {   // missing partner of an odd batch: benign +1 samples, never a premise break
-                for (int v = tid; v < N; v += nt) c2v[v].v[c] = F(1);
+                for (int v = tid; v < N; v += nt) stage[v].v[c] = F(1);
                 continue;
             }
             const uint64_t cw = a.first_cw + (uint64_t)b;
@@ -171,7 +201,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                 const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
                 for (int v = tid; v < N; v += nt) {
                     const F q = front_end<F>(y[v], a);
-                    c2v[v].v[c] = q;
+                    put(v, c, q);
                     const int cv = cvec[c] ? cvec[c][v] : 1;
                     unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
                 }
@@ -179,6 +209,32 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                 if (a.cw_table) cvec[c] = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
                 const F sigma = (F)a.sigma;
                 const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+                if (LDPC_FAST_NOB2 && !a.cw_table && !a.y_out && !a.quantize && !a.saturate && (N & 3) == 0) {
+                    // the common case in straight-line code (the all-zero codeword, no front end,
+                    // no sample output): the same values as the general loop below
+                    for (int g4 = tid; g4 * 4 < N; g4 += nt) {
+                        uint32_t u[4];
+                        philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
+                        F n[4], qv[4];
+                        box_muller(u[0], u[1], n[0], n[1]);
+                        box_muller(u[2], u[3], n[2], n[3]);
+#pragma unroll
+                        for (int q4 = 0; q4 < 4; ++q4) {
+                            qv[q4] = (F(1) + sigma * n[q4]) + F(0);   // (F)cv * (1 + sigma n) with cv = +1, then yq + 0
+                            unc[c] += (qv[q4] > F(0) ? 1 : -1) < 0;
+                            ch_ok &= dabs(qv[q4]) < kMax;
+                        }
+                        if constexpr (C == 1) {   // two ds_write_b128 (app at LDS address 0: 32-byte aligned groups)
+                            struct alignas(16) D2 { F d[2]; };
+                            lds_put<D2>(app_base + 32u * (uint32_t)g4, D2{{qv[0], qv[1]}});
+                            lds_put<D2>(app_base + 32u * (uint32_t)g4 + 16u, D2{{qv[2], qv[3]}});
+                        } else {
+#pragma unroll
+                            for (int q4 = 0; q4 < 4; ++q4) app[4 * g4 + q4].v[c] = qv[q4];
+                        }
+                    }
+                    continue;
+                }
                 for (int g4 = tid; g4 * 4 < N; g4 += nt) {
                     uint32_t u[4];
                     philox4x32_10<true>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
@@ -193,7 +249,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                             const F yv = (F)cv * (F(1) + sigma * n[q4]);
                             if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
                             const F q = front_end<F>(yv, a);
-                            c2v[v].v[c] = q;
+                            put(v, c, q);
                             unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
                         }
                     }
@@ -202,6 +258,22 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
         }
         __syncthreads();
         P yq[CPT];
+        int flag = 0;
+        if constexpr (LDPC_FAST_NOB2) {
+            if (__builtin_amdgcn_ballot_w64(!ch_ok)) {   // rare: an input past the premise bound
+                asm volatile(";");
+                if (!ch_ok) red[31] = 1;
+            }
+#pragma unroll
+            for (int i = 0; i < CPT; ++i) {   // padding slots: +0
+                yq[i] = app[LDPC_CHK(vdst(i) < N ? vdst(i) : 0, N + 2, CHK_FAST_APP_WRITE)];
+                if (vdst(i) >= N)
+#pragma unroll
+                    for (int c = 0; c < C; ++c) yq[i].v[c] = F(0);
+            }
+            // the flag raised here is read after the first check phase's barrier (or below, T = 0)
+            if (a.T == 0) __syncthreads();
+        } else {
         bool in_ok = true;
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
@@ -226,6 +298,8 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             for (int c = 0; c < C; ++c) z.v[c] = F(0);
             for (int k = dg; k < gd; ++k) c2v[LDPC_CHK(base + k * 64, EA, CHK_FAST_BIT_READ)] = z;
         }
+        flag = red[31];
+        }
         P prev[RPT][DC];   // c2v sent on each edge last iteration: +0 before the first
 #pragma unroll
         for (int r = 0; r < RPT; ++r)
@@ -234,7 +308,6 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
 #pragma unroll
                 for (int c = 0; c < C; ++c) prev[r][k].v[c] = F(0);
 
-        int flag = red[31];
         for (int it = 0; it < a.T; ++it) {
             if (__builtin_amdgcn_readfirstlane(flag) != 0) break;
             // The packed 16-bit schedule words are opaque per iteration: otherwise
@@ -331,6 +404,13 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
             const int b = grp * C + c;
             int w = 0, synd = 0;
             if (b < a.batch) {
+                if (!cvec[c] && !a.d_out) {   // the common case: errors are the posteriors not > 0
+#pragma unroll
+                    for (int i = 0; i < CPT; ++i) {
+                        const int v = vdst(i);
+                        w += (v < N && !(app[v < N ? v : 0].v[c] > F(0))) ? 1 : 0;   // :471-474
+                    }
+                } else {
 #pragma unroll
                 for (int i = 0; i < CPT; ++i) {
                     const int v = vdst(i);
@@ -340,6 +420,7 @@ __global__ __launch_bounds__(FastShape<RPT>::threads, FastShape<RPT>::waves_per_
                         w += (d != cv);
                         if (a.d_out) a.d_out[(size_t)b * N + v] = (int8_t)d;
                     }
+                }
                 }
 #pragma unroll
                 for (int r = 0; r < RPT; ++r) {   // padding edges read the +inf sentinel: parity 0
