@@ -529,7 +529,7 @@ def main():
             "metric": METRIC, "value": head["value"], "unit": "Mbit/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": head["elapsed"] / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
-            "data": "synthetic: all-zero codeword, BPSK/AWGN from on-device Philox4x32-10 + Box-Muller (fp32 transform, samples widened to fp64 for the fp64 decoder)",
+            "data": "synthetic: all-zero codeword, BPSK/AWGN from on-device Philox4x32-10 + Box-Muller (fp32 transform on the SIMD's v_log/v_sqrt/v_sin/v_cos_f32, samples widened to fp64 for the fp64 decoder)",
             "config": {"workload": f"802.11n N=1944 R1/2 QC-LDPC, NMS alpha={args.alpha}, T={args.T}, "
                                    f"{B}-codeword AWGN batch per GPU @ {args.ebn0} dB",
                        "code": "80211n_1944_r12 (N=1944, M=972, E=6966)", "batch_per_gpu": B,

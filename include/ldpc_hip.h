@@ -195,8 +195,9 @@ int  ldpc_sim_set_codewords(ldpc_ctx *ctx, const uint8_t *bits, int rows);
 /* Fused on-device Monte-Carlo of one SNR point: BPSK, AWGN with
  * sigma = sqrt(10^(-ebn0/10)/R/2) (:146-147) from counter-based
  * Philox4x32-10 keyed by (seed, stream_id, global frame index, bit index)
- * and a Box-Muller transform in fp32 (the normals widened to double for the
- * fp64 decoders), front-end, T iterations, error accounting into the context's device
+ * and a Box-Muller transform in fp32 on the SIMD's transcendental instructions
+ * (v_log/v_sqrt/v_sin/v_cos_f32; the normals widened to double for the fp64
+ * decoders), front-end, T iterations, error accounting into the context's device
  * counters. Frames first_cw .. first_cw+batch-1; the result does not depend
  * on how frames are split across calls or devices. Asynchronous.
  * frames_dev: optional DEVICE pointer [batch] of per-frame results. */
