@@ -1538,7 +1538,21 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
         app[N] = inf;
 #pragma unroll
         for (int q = 0; q < 3 * C; ++q) red[32 + q] = 0;   // block_sum_lds totals
+        red[31] = 0;   // the premise flag: cleared again by thread 0 at the end of each group
     }
+    // Padding slots of the bit-node layout hold +0 (adding +0 leaves every sum, and hence
+    // every decision, unchanged); nothing writes them after this (the channel stages into
+    // app, the check rows scatter into their own slots and the per-lane dummies).
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+        const int dg = (int)((rs.vn_info[tid * CPT + i] >> 16) & 0xffu);
+        const int base = vgb[i] + lane, gd = vgd[i];
+        P z;
+#pragma unroll
+        for (int c = 0; c < C; ++c) z.v[c] = F(0);
+        for (int k = dg; k < gd; ++k) c2v[base + k * 64] = z;
+    }
+    __syncthreads();   // the flag's first clear before any channel raises it
 
     // The second-dispatched half of the workgroup at priority 1 for the whole
     // launch (MI355X_MICROARCH "Two waves per SIMD" item 4): +0.25 % in an
@@ -1552,23 +1566,35 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
     for (int grp = blockIdx.x; grp < ngrp; grp += gridDim.x) {
         STAMP(t_start);
-        // ---- channel (:214-238), staged through the c2v area ----
-        if (tid == 0) red[31] = 0;     // fast check-node path allowed (unless an input breaks it below)
+        // ---- channel (:214-238), staged into app as yq + 0 (never -0: v2c = app - c2v then
+        // differs at most in the sign of a zero, which sgn() and |.| ignore, and the decision
+        // app > 0 is the same; the fast check node relies on it); an input outside the fast
+        // premise (|yq| >= 1e30, inf, NaN) raises the flag, which thread 0 cleared at the end
+        // of the previous group ----
         int unc[C];
+        bool ch_ok = true;
+        auto put = [&](int v, int c, F q) {
+            q = q + F(0);
+            ch_ok &= dabs(q) < F(1e30f);
+            app[v].v[c] = q;
+        };
         const int8_t *cvec[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             unc[c] = 0;
             cvec[c] = nullptr;
             const int b = grp * C + c;
-            if (b >= a.batch) continue;
+            if (b >= a.batch) {   // missing partner of an odd batch: benign +1 samples, never counted
+                for (int v = tid; v < N; v += nt) app[v].v[c] = F(1);
+                continue;
+            }
             const uint64_t cw = a.first_cw + (uint64_t)b;
             if (SRC == SRC_GIVEN) {
                 if (a.c) cvec[c] = a.c + (size_t)b * N;
                 const F *y = reinterpret_cast<const F *>(a.y) + (size_t)b * N;
                 for (int v = tid; v < N; v += nt) {
                     const F q = front_end<F>(y[v], a);
-                    c2v[v].v[c] = q;
+                    put(v, c, q);
                     const int cv = cvec[c] ? cvec[c][v] : 1;
                     unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
                 }
@@ -1576,6 +1602,26 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
                 if (a.cw_table) cvec[c] = a.cw_table + (size_t)(cw % (uint64_t)a.cw_rows) * N;
                 const F sigma = (F)a.sigma;
                 const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+                if (!a.cw_table && !a.y_out && !a.quantize && !a.saturate && (N & 3) == 0) {
+                    // the common case in straight-line code (the all-zero codeword, no front end,
+                    // no sample output): the same values as the general loop below
+                    for (int g4 = tid; g4 * 4 < N; g4 += nt) {
+                        uint32_t u[4];
+                        philox4x32_10<LDPC_ROWS_MAD64 != 0>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id,
+                                                            k0, k1, u);
+                        F n[4];
+                        box_muller(u[0], u[1], n[0], n[1]);
+                        box_muller(u[2], u[3], n[2], n[3]);
+#pragma unroll
+                        for (int q4 = 0; q4 < 4; ++q4) {
+                            const F qv = (F(1) + sigma * n[q4]) + F(0);   // (F)cv * (1 + sigma n), cv = +1; yq + 0
+                            unc[c] += (qv > F(0) ? 1 : -1) < 0;
+                            ch_ok &= dabs(qv) < F(1e30f);
+                            app[4 * g4 + q4].v[c] = qv;
+                        }
+                    }
+                    continue;
+                }
                 for (int g4 = tid; g4 * 4 < N; g4 += nt) {
                     uint32_t u[4];
                     philox4x32_10<LDPC_ROWS_MAD64 != 0>((uint32_t)g4, (uint32_t)cw, (uint32_t)(cw >> 32), a.stream_id, k0, k1, u);
@@ -1590,41 +1636,27 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
                             const F yv = (F)cv * (F(1) + sigma * n[q4]);
                             if (a.y_out) reinterpret_cast<F *>(a.y_out)[(size_t)b * N + v] = yv;
                             const F q = front_end<F>(yv, a);
-                            c2v[v].v[c] = q;
+                            put(v, c, q);
                             unc[c] += ((q > F(0) ? 1 : -1) * cv < 0);
                         }
                     }
                 }
             }
         }
-        __syncthreads();
-        P yq[CPT];
-        bool in_ok = true;   // fast premise on the inputs: |yq| < 1e30 (inf and NaN fail it)
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const P st = c2v[vdst(i) <= N ? vdst(i) : 0];
-            // yq + 0 maps -0 to +0, so app is never -0: v2c = app - c2v differs
-            // at most in the sign of a zero, which sgn() and |.| ignore, and
-            // the decision app > 0 is the same (the fast check node relies on it)
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                yq[i].v[c] = st.v[c] + F(0);
-                in_ok &= dabs(yq[i].v[c]) < F(1e30f);
-            }
-            app[vdst(i)] = yq[i];   // v2c = yq on the first pass (:364-370)
+        if (__builtin_amdgcn_ballot_w64(!ch_ok)) {   // rare: an input outside the fast premise
+            asm volatile(";");
+            if (!ch_ok) red[31] = 1;
         }
-        if (!in_ok) red[31] = 1;
         __syncthreads();
-        // Padding slots of the bit-node layout hold +0 (adding +0 leaves every
-        // sum, and hence every decision, unchanged).
+        // yq of the thread's bit slots, read back as staged (v2c = yq on the first pass,
+        // :364-370); a padding slot +0
+        P yq[CPT];
 #pragma unroll
         for (int i = 0; i < CPT; ++i) {
-            const int dg = (int)((rs.vn_info[tid * CPT + i] >> 16) & 0xffu);
-            const int base = vgb[i] + lane, gd = vgd[i];
-            P z;
+            yq[i] = app[vdst(i) < N ? vdst(i) : 0];
+            if (vdst(i) >= N)
 #pragma unroll
-            for (int c = 0; c < C; ++c) z.v[c] = F(0);
-            for (int k = dg; k < gd; ++k) c2v[base + k * 64] = z;
+                for (int c = 0; c < C; ++c) yq[i].v[c] = F(0);
         }
 
         // c2v sent on each edge last iteration: +0 before the first. RPT <= 2 keeps
@@ -1780,6 +1812,7 @@ __global__ __launch_bounds__(RowsShape<RPT>::threads, RowsShape<RPT>::waves_per_
                 if (w > 0 && a.hist) atomicAdd(&a.hist[w - 1], 1ull);
                 if (a.frame_res) a.frame_res[b] = make_int4(w, uc, sf, 0);
             }
+            red[31] = 0;   // the next group's premise flag (raised no earlier than its channel)
         }
         __syncthreads();
 #ifdef LDPC_STAMPS
