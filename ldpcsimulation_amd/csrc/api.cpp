@@ -737,6 +737,11 @@ static bool use_rows_pp(const ldpc_ctx *c, const ldpc::KernelChoice &kc, bool f6
 // persistent workgroup-per-codeword kernel (LDPC_OPT_FLOOD_MODE = 1).
 static bool use_flood_phase(const ldpc_ctx *c) { return c->opts.v[LDPC_OPT_FLOOD_MODE] != 1; }
 
+// Resident-state budget of the global layered kernel (bytes its resident codewords touch):
+// within MI355X's 256 MiB Infinity Cache with room for the schedule and the rest of the
+// working set (measured knee: 208.5 MiB fine, 216 MiB 1.2x slower; api.cpp run_kernel).
+static constexpr size_t kLayeredResidentBudget = (size_t)208 << 20;
+
 static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int schedule)
 {
     const ldpc::OptScope os(c->opts);
@@ -758,10 +763,12 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
     int gblocks = layered ? c->num_cus : 0;
     if (kc.scratch_per_block) {
         int per_cu = layered ? ldpc::layered_blocks_per_cu(f64, kc) : ldpc::blocks_per_cu(c->dg, f64, kc);
-        // Global layered kernel: one codeword per CU by default, so the
-        // resident state (DVB-S2: 256 x 583 KB) stays inside the 256 MiB
-        // Infinity Cache (2 per CU measured 1.5x slower); LDPC_OPT_LAYERED_BPC
-        // overrides (experiments).
+        // Global layered kernel: at most one codeword per CU, and no more resident
+        // codewords than the Infinity Cache holds (kLayeredResidentBudget: DVB-S2 fp64,
+        // 1.01 MB touched per codeword, runs 6.4 ms per codeword round at 184-216
+        // resident codewords and 7.6 / 8.7 / 9.3 ms at 224 / 240 / 256 -- the state
+        // spills to HBM; 2 per CU measured 1.5x slower); LDPC_OPT_LAYERED_BPC
+        // overrides both (experiments).
         if (layered) {
             const int want = c->opts.v[LDPC_OPT_LAYERED_BPC] > 0 ? c->opts.v[LDPC_OPT_LAYERED_BPC] : 1;
             per_cu = std::min(per_cu, want);
@@ -770,7 +777,15 @@ static int run_kernel(ldpc_ctx *c, const ldpc::DecodeArgs &a, bool f64, int sche
         }
         if (per_cu <= 0) per_cu = 1;
         gblocks = per_cu * c->num_cus;
+        if (layered && c->opts.v[LDPC_OPT_LAYERED_BPC] <= 0) {
+            const size_t fp = ldpc::layered_resident_bytes(c->fs, c->ls, f64);
+            gblocks = (int)std::min<size_t>((size_t)gblocks, std::max<size_t>(1, kLayeredResidentBudget / fp));
+        }
         if (gblocks > a.batch) gblocks = a.batch;
+        if (layered) {   // the same number of codeword rounds on fewer resident codewords
+            const int rounds = (a.batch + gblocks - 1) / gblocks;
+            gblocks = (a.batch + rounds - 1) / rounds;
+        }
         HIP_TRY(c->gscratch.ensure(kc.scratch_per_block * (size_t)gblocks + 65536));   // + the phase kernels' counters
     }
 #ifdef LDPC_STAMPS

@@ -115,6 +115,7 @@ hipError_t launch_layered(const DevGraph &g, const DecodeArgs &a, bool f64, cons
                           const FloodSched &fs, const LayerSched &ls, void *gscratch, int gscratch_blocks,
                           hipStream_t s);
 int layered_blocks_per_cu(bool f64, const KernelChoice &kc);
+size_t layered_resident_bytes(const FloodSched &fs, const LayerSched &ls, bool f64);
 // Packed check state of the flood and layered kernels: a 5-bit argmin and one
 // sign bit per edge in a 32-bit meta word.
 constexpr int kPackedMaxDc = 26;

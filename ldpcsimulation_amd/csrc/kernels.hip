@@ -1081,7 +1081,8 @@ hipError_t launch_flood_phase(const DevGraph &g, const FloodSched &fs, const Dec
 // one thread per row, with a workgroup barrier between layers. One workgroup
 // per codeword (persistent over the batch). State:
 //   app[NP + 1]            posteriors in layered position order (app[NP] = +inf pad)
-//   m12[M_pad], meta[M_pad] the packed check state as in k_decode_flood
+//   m12[M_pad], meta[M_pad] the packed check state as in k_decode_flood (meta:
+//                          argmin | signs << 5, 16 bits for rows of degree <= 8)
 // -- in LDS when it fits (k_decode_layered_lds) or in a per-workgroup global
 // slot (k_decode_layered_global: DVB-S2's 583 KB), where in fp64 positions [0, P) --
 // the highest-degree bits, LayerSchedule::pos_of_bit -- stay in LDS (LayApp).
@@ -1246,11 +1247,45 @@ __device__ __forceinline__ uint32_t layered_row(const DecodeArgs &a, int deg, ty
     return (uint32_t)amin | (eff << 5);
 }
 
+// Layered check state: argmin (5 bits) | signs << 5 -- 16 bits for the DC = 8 instantiation
+// (fs.dc <= 8, launch_layered_dc), 32 above (2 B less state per row: DVB-S2
+// 65 KB per codeword, more resident codewords inside the Infinity Cache).
+template <int DC> using LayMeta = typename std::conditional<(DC <= 8), uint16_t, uint32_t>::type;
+__host__ __device__ inline size_t layered_meta_bytes(const FloodSched &fs) { return fs.dc <= 8 ? 2 : 4; }
+
+// Diagnostic builds (-DLDPC_STAMPS, `make variant`; scripts/lay_stamp_run.sh): per wave,
+// s_memtime cycles of the layered kernel's phases, each closed by a wait on its memory
+// operations (0 schedule loads, 1 posterior gathers + check state, 2 check rule, 6 scatter
+// issue, 3 scatter drain, 4 layer barrier, 5 channel, init, decisions and accounting;
+// 7 counts the passes), to a.stamps[(block*16+wave)*8 + k].
+struct LayStamps {
+#ifdef LDPC_STAMPS
+    unsigned long long t0 = __builtin_amdgcn_s_memtime(), acc[8] = {};
+    __device__ __forceinline__ void mark(int k, bool drain = false)
+    {
+        if (drain) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        acc[k] += t - t0;
+        t0 = t;
+    }
+    __device__ __forceinline__ void pass() { acc[7] += 1; }
+    __device__ __forceinline__ void out(const DecodeArgs &a) const
+    {
+        if (a.stamps && (threadIdx.x & 63) == 0 && blockIdx.x < 256)
+            for (int k = 0; k < 8; ++k) a.stamps[(blockIdx.x * 16 + (threadIdx.x >> 6)) * 8 + k] = acc[k];
+    }
+#else
+    __device__ __forceinline__ void mark(int, bool = false) {}
+    __device__ __forceinline__ void pass() {}
+    __device__ __forceinline__ void out(const DecodeArgs &) const {}
+#endif
+};
+
 template <typename F, int SRC, int DC, int R, bool SPLIT>
 __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const DevGraph &g, const FloodSched &fs,
                                                   const LayerSched &ls, int b, const LayApp<F, SPLIT> &app,
-                                                  typename F2T<F>::T *m12, uint32_t *meta, int *red,
-                                                  unsigned long long *acc)
+                                                  typename F2T<F>::T *m12, LayMeta<DC> *meta, int *red,
+                                                  unsigned long long *acc, LayStamps &st)
 {
     using F2 = typename F2T<F>::T;
     const int tid = threadIdx.x, nt = blockDim.x;
@@ -1273,6 +1308,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
         meta[i] = 0;
     }
     __syncthreads();
+    st.mark(5);
 
     for (int it = 0; it < a.T; ++it) {
         for (int L = 0; L < ls.nlayers; ++L) {
@@ -1291,6 +1327,8 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
 #pragma unroll
                     for (int k = 0; k < DC; ++k)
                         sp[r][k] = k < deg[r] ? LDPC_CHK(ls.sp[(size_t)k * MP + i0 + r * nt], NP + 1, CHK_FLOOD_APP) : NP;
+                st.pass();
+                st.mark(0, true);
 #pragma unroll
                 for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -1302,20 +1340,25 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
                         om[r] = meta[i0 + r * nt];
                     }
                 }
+                st.mark(1, true);
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     if (deg[r]) {
                         F2 nw;
                         const uint32_t nm = layered_row<F, DC>(a, deg[r], old[r], om[r], xs[r], alpha, delta, nw);
+                        st.mark(2);
                         m12[i0 + r * nt] = nw;
-                        meta[i0 + r * nt] = nm;
+                        meta[i0 + r * nt] = (LayMeta<DC>)nm;
 #pragma unroll
                         for (int k = 0; k < DC; ++k)
                             if (k < deg[r]) app.st(sp[r][k], xs[r][k]);   // posterior update
                     }
                 }
+                st.mark(6);
+                st.mark(3, true);
             }
             __syncthreads();
+            st.mark(4);
         }
     }
 
@@ -1346,6 +1389,7 @@ __device__ __forceinline__ void decode_layered_cw(const DecodeArgs &a, const Dev
         if (a.frame_res) a.frame_res[b] = make_int4(sums[0], sums[1], sf, 0);
     }
     __syncthreads();
+    st.mark(5);
 }
 
 __device__ __forceinline__ void flush_acc(const DecodeArgs &a, unsigned long long *acc)
@@ -1364,7 +1408,7 @@ __host__ __device__ inline size_t layered_m12_off(const FloodSched &fs, size_t f
 }
 __host__ __device__ inline size_t layered_state_bytes(const FloodSched &fs, const LayerSched &ls, size_t fsz)
 {
-    return (layered_m12_off(fs, fsz) + (size_t)ls.M_pad * (2 * fsz + 4) + 255) & ~(size_t)255;
+    return (layered_m12_off(fs, fsz) + (size_t)ls.M_pad * (2 * fsz + layered_meta_bytes(fs)) + 255) & ~(size_t)255;
 }
 
 template <typename F, int SRC, int DC, int R>
@@ -1376,15 +1420,17 @@ __global__ __launch_bounds__(512) void k_decode_layered_lds(DecodeArgs a, DevGra
     __shared__ unsigned long long acc[6];
     F *app = reinterpret_cast<F *>(smem);
     F2 *m12 = reinterpret_cast<F2 *>(smem + layered_m12_off(fs, sizeof(F)));
-    uint32_t *meta = reinterpret_cast<uint32_t *>(m12 + ls.M_pad);
+    LayMeta<DC> *meta = reinterpret_cast<LayMeta<DC> *>(m12 + ls.M_pad);
     if (threadIdx.x == 0) {
         app[fs.ngroups * 64] = dinf<F>();
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
     }
     const LayApp<F, false> la{app, buf_rsrc(app, 0), 0};
+    LayStamps st;
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
-        decode_layered_cw<F, SRC, DC, R, false>(a, g, fs, ls, b, la, m12, meta, red, acc);
+        decode_layered_cw<F, SRC, DC, R, false>(a, g, fs, ls, b, la, m12, meta, red, acc, st);
+    st.out(a);
     flush_acc(a, acc);
 }
 // State in a global slot; SPLIT (fp64): except the posteriors of layered
@@ -1402,7 +1448,7 @@ __global__ __launch_bounds__(NT) void k_decode_layered_global(DecodeArgs a, DevG
     unsigned char *base = scratch + slot_bytes * blockIdx.x;
     F *app = reinterpret_cast<F *>(base);
     F2 *m12 = reinterpret_cast<F2 *>(base + layered_m12_off(fs, sizeof(F)));
-    uint32_t *meta = reinterpret_cast<uint32_t *>(m12 + ls.M_pad);
+    LayMeta<DC> *meta = reinterpret_cast<LayMeta<DC> *>(m12 + ls.M_pad);
     const LayApp<F, SPLIT> la{SPLIT ? reinterpret_cast<F *>(smem) : app,
                               buf_rsrc(app, (uint32_t)layered_m12_off(fs, sizeof(F))), P};
     if (threadIdx.x == 0) {
@@ -1410,8 +1456,10 @@ __global__ __launch_bounds__(NT) void k_decode_layered_global(DecodeArgs a, DevG
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[q] = 0;
     }
+    LayStamps st;
     for (int b = blockIdx.x; b < a.batch; b += gridDim.x)
-        decode_layered_cw<F, SRC, DC, R, SPLIT>(a, g, fs, ls, b, la, m12, meta, red, acc);
+        decode_layered_cw<F, SRC, DC, R, SPLIT>(a, g, fs, ls, b, la, m12, meta, red, acc, st);
+    st.out(a);
     flush_acc(a, acc);
 }
 
@@ -2209,6 +2257,17 @@ hipError_t launch_layered(const DevGraph &g, const DecodeArgs &a, bool f64, cons
                                   : launch_layered_dc<double, SRC_PHILOX>(a, g, kc, fs, ls, gscratch, gscratch_blocks, s);
     return a.src == SRC_GIVEN ? launch_layered_dc<float, SRC_GIVEN>(a, g, kc, fs, ls, gscratch, gscratch_blocks, s)
                               : launch_layered_dc<float, SRC_PHILOX>(a, g, kc, fs, ls, gscratch, gscratch_blocks, s);
+}
+
+// Bytes of its global slot one resident codeword of the global layered kernel touches:
+// the posteriors outside LDS (fp64: positions [P, NP]; fp32: all) and the packed check
+// state (min1/min2 + meta per row). DVB-S2 N=64800: 1.01 MB fp64, 0.65 MB fp32.
+size_t layered_resident_bytes(const FloodSched &fs, const LayerSched &ls, bool f64)
+{
+    const long np1 = (long)fs.ngroups * 64 + 1;
+    const size_t fsz = f64 ? 8 : 4;
+    const long P = f64 ? layered_lds_positions((int)np1, 8) : 0;
+    return (size_t)(np1 - P) * fsz + (size_t)ls.M_pad * (2 * fsz + layered_meta_bytes(fs));
 }
 
 int layered_blocks_per_cu(bool f64, const KernelChoice &kc)

@@ -165,6 +165,25 @@ def test_dvbs2_layered_decisions_vs_oracle(gpu_ctx_factory, prec):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_dvbs2_layered_frames_independent_of_grid(prec):
+    """The global layered kernel sizes its grid to the batch (resident codewords inside the
+    Infinity Cache, the same number of codeword rounds on fewer blocks, api.cpp run_kernel):
+    every codeword's result is the same in one 461-frame launch (3 rounds on 154 blocks) as
+    in launches of 1, 230 (one round) and 230 frames."""
+    native = _native()
+    g = native.Graph.from_alist(code_path("dvbs2_1_2.alist"))
+    ctx = native.Context(g, 0, 461)
+    cfg = native.DecoderConfig(variant=native.NMS, alpha=1.25, T=3, schedule=native.LAYERED,
+                               precision=native.F64 if prec == "f64" else native.F32)
+    assert ctx.kernel_info(cfg)["kernel"] == "layered_global"
+    whole, cw = ctx.sim_batch(0.9, 0.5, cfg, 11, 2, 5, 461)
+    parts = [ctx.sim_batch(0.9, 0.5, cfg, 11, 2, 5 + f, n)[0] for f, n in ((0, 1), (1, 230), (231, 230))]
+    assert np.array_equal(whole, np.concatenate(parts))
+    assert cw.frames == 461 and int(whole["bit_err"].sum()) > 0
+
+
+@pytest.mark.gpu
 def test_dvbs2_layered_beats_flooding_fer():
     """Config 3 sanity at 1.0 dB, T=50 (NMS a=1.25): the layered FER is well below the flooding
     FER on the same frames (measured 194 vs 1212 of 2048)."""
