@@ -266,7 +266,8 @@ typedef enum {
     LDPC_OPT_FLOOD_RESIDENT = 9,   /* phase flooding: resident codewords (0 = sized to the Infinity Cache)    */
     LDPC_OPT_FLOOD_STREAMS = 10,   /* phase flooding: 2 = the resident set in two halves on two streams       */
     LDPC_OPT_FLOOD_BPC = 11,       /* persistent flooding kernel: blocks per CU cap (0 = occupancy)           */
-    LDPC_OPT_LAYERED_BPC = 12,     /* global layered kernel: blocks per CU (0 = 1)                            */
+    LDPC_OPT_LAYERED_BPC = 12,     /* global layered kernel: blocks per CU (0 = 1, capped by the 208 MiB      */
+                                   /* resident-state budget; set: that many per CU, no cap)                  */
     LDPC_OPT_LAYERED_LDS_POS = 13, /* global layered kernel: positions kept in LDS + 1 (0 = as many as fit)   */
     LDPC_OPT_LAYERED_ROWS64 = 14,  /* 512-thread global layered kernel, fp64 rows per pass: 1 or 2 (0 = 2)    */
     LDPC_OPT_LAYERED_THREADS = 15, /* global layered kernel threads: 512 or 1024 (0 = 1024)                   */
